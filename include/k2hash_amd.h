@@ -1,0 +1,116 @@
+/*
+ * k2hash_amd -- MI355X-native key-hash path for yahoojapan/k2hash.
+ *
+ * C ABI of the two shared libraries built from k2hash_amd/csrc/:
+ *
+ *   libk2hfnv_plugin.so   the DROP-IN hash plugin.  Exports exactly the three
+ *                         symbols k2hash's plugin loader resolves (section 1).
+ *                         Pure C++, no HIP dependency, safe to dlopen from any
+ *                         process/thread and across fork.
+ *   libk2hash_amd.so      the same three symbols plus the batch ABI (section 2)
+ *                         backed by hand-written CDNA4 HIP kernels.  Also a valid
+ *                         plugin; HIP is initialised lazily by the first batch call.
+ *
+ * All hashes are bit-identical to the reference's default build
+ * (lib/k2hashfunc.cc, "FNV-1A BUILTIN"), or, with K2H_AMD_FLAG_STD_FNV, to its
+ * USE_STD_FNV_HASH_FUNCTION build ("STD::FNV BUILTIN").
+ */
+#ifndef K2HASH_AMD_H
+#define K2HASH_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* lib/k2hash.h:37 */
+typedef uint64_t k2h_hash_t;
+
+/* ---------------------------------------------------------------------------
+ * 1. Drop-in plugin ABI.
+ *
+ * Replaces the weak builtins declared at lib/k2hashfunc.h:62-74 and defined at
+ * lib/k2hashfunc.cc:62-96.  K2HashDynLib::Load (lib/k2hashfunc.cc:132-161,
+ * reached from k2h_load_hash_library, lib/k2hash.cc:106-117, and from the tools'
+ * -ext options, e.g. tests/k2hlinetool.cc:4995-5008) dlopen()s the plugin with
+ * RTLD_LAZY and dlsym()s these three names, all-or-nothing
+ * (lib/k2hashfunc.cc:149-156).  The same symbols also override the builtins at
+ * link time or through LD_PRELOAD (lib/k2hcommon.h:41-45, docs/k2hash.1:50-55).
+ *
+ * Semantics (identical to the reference):
+ *   - ptr == NULL or length == 0 -> 0            (lib/k2hashfunc.cc:66-68, 80-82)
+ *   - k2h_hash: FNV-1a-64 over `length` bytes, each byte read as signed char
+ *     and sign-extended before the XOR               (lib/k2hashfunc.cc:49-59)
+ *   - k2h_second_hash: same over length-1 bytes when length > 1
+ *                                                     (lib/k2hashfunc.cc:83-85)
+ *   - k2h_hash_version: "FNV-1A BUILTIN" -- the reference's own string, because
+ *     the hashes are identical and the string is stamped into / checked against
+ *     every k2hash file header (lib/k2hshminit.cc:405, 641-646).  < 32 bytes
+ *     (lib/k2hash.h:69).
+ * Reentrant, lock-free, allocation-free, never throws or logs; no GPU work.
+ * ------------------------------------------------------------------------- */
+k2h_hash_t k2h_hash(const void* ptr, size_t length);        /* lib/k2hashfunc.h:65 */
+k2h_hash_t k2h_second_hash(const void* ptr, size_t length); /* lib/k2hashfunc.h:68 */
+const char* k2h_hash_version(void);                         /* lib/k2hashfunc.h:72 */
+
+/* ---------------------------------------------------------------------------
+ * 2. Batch ABI (new surface; libk2hash_amd.so only).
+ *
+ * The reference has no batch entry point: every call site hashes one key
+ * synchronously (lib/k2hshm.cc:1230-1231, 2184-2185, ...).  Bulk callers
+ * (bulk loads, archive import, RALLEDATA producers, benches) use these.
+ *
+ * Return value: K2H_AMD_OK (0) or a negative K2H_AMD_E* code;
+ * k2h_amd_strerror() describes the last failure on the calling thread.
+ * Per-key results follow the plugin semantics above; a key of length 0 hashes
+ * to 0 (h1 and h2), and so does every key when the byte buffer is NULL.
+ * h2 may be NULL (second hash not wanted).  `stream` is a hipStream_t
+ * (NULL = the null stream); device-pointer calls are asynchronous on it.
+ * ------------------------------------------------------------------------- */
+#define K2H_AMD_OK 0
+#define K2H_AMD_EINVAL (-1)   /* bad argument (NULL output, overflow, ...) */
+#define K2H_AMD_EHIP (-2)     /* HIP runtime error (see k2h_amd_strerror) */
+#define K2H_AMD_ENOMEM (-3)   /* device / pinned host allocation failed */
+#define K2H_AMD_ENODEV (-4)   /* no usable gfx950 device */
+
+#define K2H_AMD_FLAG_STD_FNV 0x1u /* USE_STD_FNV_HASH_FUNCTION build: seed 2166136261
+                                      (lib/k2hashfunc.cc:35-37, 69-70, 86-87) */
+
+/* Fixed-length keys in device memory: key i = keys[i*key_len, (i+1)*key_len). */
+int k2h_amd_hash_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t* h1, uint64_t* h2, uint32_t flags,
+                       void* stream);
+
+/* CSR keys in device memory: key i = bytes[offsets[i], offsets[i+1]), offsets has n+1
+ * non-decreasing entries (byte offsets relative to `bytes`). */
+int k2h_amd_hash_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1, uint64_t* h2,
+                     uint32_t flags, void* stream);
+
+/* Host-memory forms: same layouts, host pointers in and out.  The library stages
+ * through pinned buffers and overlaps H2D / kernel / D2H in chunks on `device`.
+ * Synchronous: returns when h1/h2 are filled. */
+int k2h_amd_hash_fixed_host(const void* keys, uint64_t key_len, uint64_t n, uint64_t* h1, uint64_t* h2,
+                            uint32_t flags, int device);
+int k2h_amd_hash_csr_host(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1, uint64_t* h2,
+                          uint32_t flags, int device);
+
+/* Identity / diagnostics. */
+const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */
+const char* k2h_amd_strerror(int code); /* message for `code`, with the last HIP error if any */
+int k2h_amd_set_variant(int variant);   /* A/B knob for measurement; 0 = auto (default) */
+int k2h_amd_get_variant(void);
+
+/* Synthetic-workload generator used by bench.py and the tests (not the hash
+ * path): writes bytes [byte_off, byte_off+nbytes) of the splitmix64 word stream
+ * with `seed`, and CSR lengths min_len + mix(seed, first_key+i) % (max_len-min_len+1).
+ * Same spec as oracle/fnv_oracle.c. */
+int k2h_amd_synth_bytes(void* out, uint64_t nbytes, uint64_t seed, uint64_t byte_off, void* stream);
+int k2h_amd_synth_lengths(uint32_t* lens, uint64_t n, uint64_t seed, uint64_t first_key, uint32_t min_len,
+                          uint32_t max_len, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* K2HASH_AMD_H */

@@ -1,0 +1,164 @@
+"""Batch key hashing on MI355X through the k2hash_amd C ABI.
+
+Device forms take torch tensors already resident in HBM and launch on the
+current torch stream; host forms take numpy arrays and use the library's
+pinned-staging pipeline.  Hashes are returned as int64 tensors/arrays holding
+the 64-bit k2h_hash_t bit patterns (view as uint64 with numpy for printing).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+
+from . import _native
+
+FLAG_STD_FNV = _native.K2H_AMD_FLAG_STD_FNV
+
+
+def _torch():
+    import torch  # deferred: host-only users need not import torch
+
+    return torch
+
+
+def _stream_handle(stream=None) -> ctypes.c_void_p:
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def _dev_ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _check_dev(t, name: str, dtype) -> None:
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def hash_fixed(keys, key_len: int, second: bool = False, std_fnv: bool = False,
+               out: Optional[Tuple] = None, stream=None):
+    """Hash n = keys.numel() // key_len fixed-length keys held in a uint8 device tensor.
+
+    Returns (h1, h2) int64 device tensors (h2 None unless second=True).
+    """
+    torch = _torch()
+    _check_dev(keys, "keys", torch.uint8)
+    if key_len <= 0:
+        raise ValueError("key_len must be positive")
+    n = keys.numel() // key_len
+    if out is not None:
+        h1, h2 = out
+    else:
+        h1 = torch.empty(n, dtype=torch.int64, device=keys.device)
+        h2 = torch.empty(n, dtype=torch.int64, device=keys.device) if second else None
+    flags = FLAG_STD_FNV if std_fnv else 0
+    rc = _native.batch_lib().k2h_amd_hash_fixed(
+        _dev_ptr(keys), key_len, n, _dev_ptr(h1), _dev_ptr(h2) if h2 is not None else None, flags,
+        _stream_handle(stream))
+    _native.check(rc)
+    return h1, h2
+
+
+def hash_csr(data, offsets, second: bool = False, std_fnv: bool = False, out: Optional[Tuple] = None,
+             stream=None):
+    """Hash CSR keys: key i = data[offsets[i]:offsets[i+1]] (uint8 / int64 device tensors)."""
+    torch = _torch()
+    _check_dev(data, "data", torch.uint8)
+    _check_dev(offsets, "offsets", torch.int64)
+    n = offsets.numel() - 1
+    if n < 0:
+        raise ValueError("offsets must have n+1 entries")
+    if out is not None:
+        h1, h2 = out
+    else:
+        h1 = torch.empty(n, dtype=torch.int64, device=data.device)
+        h2 = torch.empty(n, dtype=torch.int64, device=data.device) if second else None
+    flags = FLAG_STD_FNV if std_fnv else 0
+    base = _dev_ptr(data) if data.numel() > 0 else ctypes.c_void_p(data.data_ptr() or 1)
+    rc = _native.batch_lib().k2h_amd_hash_csr(
+        base, _dev_ptr(offsets), n, _dev_ptr(h1), _dev_ptr(h2) if h2 is not None else None, flags,
+        _stream_handle(stream))
+    _native.check(rc)
+    return h1, h2
+
+
+def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def hash_fixed_host(keys: np.ndarray, key_len: int, second: bool = False, std_fnv: bool = False,
+                    device: int = 0):
+    """Host-memory form of hash_fixed (numpy uint8 in, numpy uint64 out)."""
+    keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+    n = keys.size // key_len
+    h1 = np.empty(n, dtype=np.uint64)
+    h2 = np.empty(n, dtype=np.uint64) if second else None
+    rc = _native.batch_lib().k2h_amd_hash_fixed_host(
+        _np_ptr(keys), key_len, n, _np_ptr(h1), _np_ptr(h2) if h2 is not None else None,
+        FLAG_STD_FNV if std_fnv else 0, device)
+    _native.check(rc)
+    return h1, h2
+
+
+def hash_csr_host(data: np.ndarray, offsets: np.ndarray, second: bool = False, std_fnv: bool = False,
+                  device: int = 0):
+    """Host-memory form of hash_csr."""
+    data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    offsets = np.ascontiguousarray(offsets, dtype=np.uint64).reshape(-1)
+    n = offsets.size - 1
+    h1 = np.empty(n, dtype=np.uint64)
+    h2 = np.empty(n, dtype=np.uint64) if second else None
+    dptr = _np_ptr(data) if data.size else ctypes.c_void_p(1)
+    rc = _native.batch_lib().k2h_amd_hash_csr_host(
+        dptr, _np_ptr(offsets), n, _np_ptr(h1), _np_ptr(h2) if h2 is not None else None,
+        FLAG_STD_FNV if std_fnv else 0, device)
+    _native.check(rc)
+    return h1, h2
+
+
+# ----------------------------------------------------------------------------
+# Synthetic workloads (bench/test harness): splitmix64 counter stream, same spec
+# as oracle/fnv_oracle.c.  Generated on the device.
+# ----------------------------------------------------------------------------
+SEED_BYTES = 0x6B32686173680001
+SEED_LENS = 0x6B32686173680002
+
+
+def synth_bytes(nbytes: int, device, seed: int = SEED_BYTES, byte_off: int = 0, stream=None):
+    torch = _torch()
+    t = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    rc = _native.batch_lib().k2h_amd_synth_bytes(_dev_ptr(t), nbytes, seed, byte_off, _stream_handle(stream))
+    _native.check(rc)
+    return t
+
+
+def synth_offsets(n: int, device, min_len: int = 8, max_len: int = 256, seed: int = SEED_LENS,
+                  first_key: int = 0, stream=None):
+    """CSR offsets (n+1, int64, starting at 0) for keys first_key .. first_key+n-1."""
+    torch = _torch()
+    lens = torch.empty(n, dtype=torch.int32, device=device)
+    rc = _native.batch_lib().k2h_amd_synth_lengths(_dev_ptr(lens), n, seed, first_key, min_len, max_len,
+                                                    _stream_handle(stream))
+    _native.check(rc)
+    off = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    torch.cumsum(lens, dim=0, dtype=torch.int64, out=off[1:])
+    return off
+
+
+def set_variant(v: int) -> int:
+    return _native.batch_lib().k2h_amd_set_variant(v)
+
+
+def get_variant() -> int:
+    return _native.batch_lib().k2h_amd_get_variant()
+
+
+def version() -> str:
+    return _native.batch_lib().k2h_amd_version().decode()

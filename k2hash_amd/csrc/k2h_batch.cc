@@ -1,0 +1,288 @@
+// k2hash_amd -- batch C-ABI (include/k2hash_amd.h section 2) over the HIP kernels.
+//
+// Device-pointer entry points validate arguments and launch on the caller's stream.
+// Host-pointer entry points stage through pinned buffers and pipeline
+// host-copy -> H2D -> kernel -> D2H over two streams in chunks, so a caller that holds
+// keys in host memory (the k2hash process itself) gets the PCIe-bound rate without
+// managing device memory.  HIP is touched only inside these calls (lazy init), never at
+// library load, so libk2hash can dlopen this library as its plugin safely.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+
+#include "../../include/k2hash_amd.h"
+#include "k2h_kernels.h"
+
+namespace {
+
+thread_local char g_err[256];
+int g_variant = -1;  // -1: read K2H_AMD_VARIANT once
+
+int variant() {
+  if (g_variant < 0) {
+    const char* v = getenv("K2H_AMD_VARIANT");
+    g_variant = v ? atoi(v) : 0;
+  }
+  return g_variant;
+}
+
+int fail(int code, const char* what, hipError_t e = hipSuccess) {
+  if (e != hipSuccess)
+    snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
+  else
+    snprintf(g_err, sizeof g_err, "%s", what);
+  return code;
+}
+
+uint64_t seed_for(uint32_t flags) {
+  return (flags & K2H_AMD_FLAG_STD_FNV) ? k2h::kSeedStdValue : k2h::kSeedBuiltinValue;
+}
+
+// ---------------------------------------------------------------------------
+// Host-path staging context: per device, two pipeline slots.
+// ---------------------------------------------------------------------------
+struct Slot {
+  hipStream_t stream = nullptr;
+  hipEvent_t done = nullptr;
+  uint8_t* h_in = nullptr;   // pinned input bytes
+  uint64_t* h_off = nullptr; // pinned rebased offsets (CSR)
+  uint64_t* h_out = nullptr; // pinned h1 (+h2) results
+  uint8_t* d_in = nullptr;
+  uint64_t* d_off = nullptr;
+  uint64_t* d_out = nullptr;
+  uint64_t cap_in = 0, cap_keys = 0;
+  bool busy = false;
+  // pending result copy-out
+  uint64_t first = 0, count = 0;
+  bool want_h2 = false;
+};
+
+struct HostCtx {
+  std::mutex mu;
+  int device = -1;
+  Slot slot[2];
+};
+
+HostCtx g_ctx[64];
+
+int slot_reserve(Slot& s, uint64_t bytes, uint64_t keys) {
+  hipError_t e;
+  if (!s.stream) {
+    if ((e = hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking)) != hipSuccess)
+      return fail(K2H_AMD_EHIP, "hipStreamCreate", e);
+    if ((e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess)
+      return fail(K2H_AMD_EHIP, "hipEventCreate", e);
+  }
+  if (bytes > s.cap_in) {
+    if (s.h_in) (void)hipHostFree(s.h_in);
+    if (s.d_in) (void)hipFree(s.d_in);
+    s.h_in = nullptr;
+    s.d_in = nullptr;
+    s.cap_in = 0;
+    if (hipHostMalloc((void**)&s.h_in, bytes, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc((void**)&s.d_in, bytes) != hipSuccess)
+      return fail(K2H_AMD_ENOMEM, "staging allocation (bytes)");
+    s.cap_in = bytes;
+  }
+  if (keys > s.cap_keys) {
+    if (s.h_off) (void)hipHostFree(s.h_off);
+    if (s.h_out) (void)hipHostFree(s.h_out);
+    if (s.d_off) (void)hipFree(s.d_off);
+    if (s.d_out) (void)hipFree(s.d_out);
+    s.h_off = nullptr;
+    s.h_out = nullptr;
+    s.d_off = nullptr;
+    s.d_out = nullptr;
+    s.cap_keys = 0;
+    if (hipHostMalloc((void**)&s.h_off, (keys + 1) * 8, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&s.h_out, keys * 16, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc((void**)&s.d_off, (keys + 1) * 8) != hipSuccess || hipMalloc((void**)&s.d_out, keys * 16) != hipSuccess)
+      return fail(K2H_AMD_ENOMEM, "staging allocation (keys)");
+    s.cap_keys = keys;
+  }
+  return K2H_AMD_OK;
+}
+
+// Wait for a slot's previous chunk and copy its results out of pinned memory.
+int slot_drain(Slot& s, uint64_t* h1, uint64_t* h2) {
+  if (!s.busy) return K2H_AMD_OK;
+  hipError_t e = hipEventSynchronize(s.done);
+  s.busy = false;
+  if (e != hipSuccess) return fail(K2H_AMD_EHIP, "chunk completion", e);
+  memcpy(h1 + s.first, s.h_out, s.count * 8);
+  if (s.want_h2 && h2) memcpy(h2 + s.first, s.h_out + s.count, s.count * 8);
+  return K2H_AMD_OK;
+}
+
+constexpr uint64_t kChunkBytes = 64ull << 20;  // 64 MiB of key bytes per pipeline chunk
+constexpr uint64_t kChunkKeysMax = 4ull << 20;
+
+int set_device(int device) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess || count == 0) return fail(K2H_AMD_ENODEV, "no HIP device", e);
+  if (device < 0 || device >= count || device >= 64) return fail(K2H_AMD_EINVAL, "device index out of range");
+  if ((e = hipSetDevice(device)) != hipSuccess) return fail(K2H_AMD_EHIP, "hipSetDevice", e);
+  return K2H_AMD_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) int k2h_amd_hash_fixed(const void* keys, uint64_t key_len, uint64_t n,
+                                                              uint64_t* h1, uint64_t* h2, uint32_t flags,
+                                                              void* stream) {
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1) return fail(K2H_AMD_EINVAL, "h1 is NULL");
+  if (key_len && n > UINT64_MAX / key_len) return fail(K2H_AMD_EINVAL, "n * key_len overflows");
+  hipError_t e = k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream);
+  if (e != hipSuccess) return fail(K2H_AMD_EHIP, "launch_fixed", e);
+  return K2H_AMD_OK;
+}
+
+__attribute__((visibility("default"))) int k2h_amd_hash_csr(const void* bytes, const uint64_t* offsets, uint64_t n,
+                                                            uint64_t* h1, uint64_t* h2, uint32_t flags,
+                                                            void* stream) {
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1 || !offsets) return fail(K2H_AMD_EINVAL, "h1/offsets is NULL");
+  hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream);
+  if (e != hipSuccess) return fail(K2H_AMD_EHIP, "launch_csr", e);
+  return K2H_AMD_OK;
+}
+
+__attribute__((visibility("default"))) int k2h_amd_hash_fixed_host(const void* keys, uint64_t key_len, uint64_t n,
+                                                                   uint64_t* h1, uint64_t* h2, uint32_t flags,
+                                                                   int device) {
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1) return fail(K2H_AMD_EINVAL, "h1 is NULL");
+  if (key_len && n > UINT64_MAX / key_len) return fail(K2H_AMD_EINVAL, "n * key_len overflows");
+  if (!keys || key_len == 0) {
+    memset(h1, 0, n * 8);
+    if (h2) memset(h2, 0, n * 8);
+    return K2H_AMD_OK;
+  }
+  int rc = set_device(device);
+  if (rc) return rc;
+  HostCtx& c = g_ctx[device];
+  std::lock_guard<std::mutex> lk(c.mu);
+  uint64_t per = kChunkBytes / key_len;
+  if (per == 0) per = 1;
+  if (per > kChunkKeysMax) per = kChunkKeysMax;
+  const uint8_t* src = (const uint8_t*)keys;
+  int k = 0;
+  for (uint64_t first = 0; first < n; first += per, k ^= 1) {
+    uint64_t cnt = n - first < per ? n - first : per;
+    Slot& s = c.slot[k];
+    if ((rc = slot_drain(s, h1, h2))) return rc;
+    if ((rc = slot_reserve(s, per * key_len, per))) return rc;
+    memcpy(s.h_in, src + first * key_len, cnt * key_len);
+    hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, cnt * key_len, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = k2h::launch_fixed(s.d_in, key_len, cnt, seed_for(flags), s.d_out, h2 ? s.d_out + cnt : nullptr, variant(),
+                            s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, cnt * (h2 ? 16 : 8), hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "fixed host chunk", e);
+    s.busy = true;
+    s.first = first;
+    s.count = cnt;
+    s.want_h2 = h2 != nullptr;
+  }
+  for (int j = 0; j < 2; ++j)
+    if ((rc = slot_drain(c.slot[j], h1, h2))) return rc;
+  return K2H_AMD_OK;
+}
+
+__attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* bytes, const uint64_t* offsets,
+                                                                 uint64_t n, uint64_t* h1, uint64_t* h2,
+                                                                 uint32_t flags, int device) {
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1 || !offsets) return fail(K2H_AMD_EINVAL, "h1/offsets is NULL");
+  if (!bytes) {
+    memset(h1, 0, n * 8);
+    if (h2) memset(h2, 0, n * 8);
+    return K2H_AMD_OK;
+  }
+  for (uint64_t i = 0; i < n; ++i)
+    if (offsets[i + 1] < offsets[i]) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
+  int rc = set_device(device);
+  if (rc) return rc;
+  HostCtx& c = g_ctx[device];
+  std::lock_guard<std::mutex> lk(c.mu);
+  const uint8_t* src = (const uint8_t*)bytes;
+  int k = 0;
+  uint64_t first = 0;
+  while (first < n) {
+    // grow the chunk by keys until the byte budget or the key cap is reached (always >= 1 key)
+    uint64_t last = first + 1;
+    uint64_t cap_keys = first + kChunkKeysMax < n ? first + kChunkKeysMax : n;
+    while (last < cap_keys && offsets[last + 1] - offsets[first] <= kChunkBytes) ++last;
+    uint64_t cnt = last - first;
+    uint64_t nb = offsets[last] - offsets[first];
+    Slot& s = c.slot[k];
+    if ((rc = slot_drain(s, h1, h2))) return rc;
+    if ((rc = slot_reserve(s, nb > kChunkBytes ? nb : kChunkBytes, kChunkKeysMax))) return rc;
+    memcpy(s.h_in, src + offsets[first], nb);
+    for (uint64_t i = 0; i <= cnt; ++i) s.h_off[i] = offsets[first + i] - offsets[first];
+    hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, nb, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice, s.stream);
+    if (e == hipSuccess)
+      e = k2h::launch_csr(s.d_in, s.d_off, cnt, seed_for(flags), s.d_out, h2 ? s.d_out + cnt : nullptr, variant(),
+                          s.stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, cnt * (h2 ? 16 : 8), hipMemcpyDeviceToHost, s.stream);
+    if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
+    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "csr host chunk", e);
+    s.busy = true;
+    s.first = first;
+    s.count = cnt;
+    s.want_h2 = h2 != nullptr;
+    first = last;
+    k ^= 1;
+  }
+  for (int j = 0; j < 2; ++j)
+    if ((rc = slot_drain(c.slot[j], h1, h2))) return rc;
+  return K2H_AMD_OK;
+}
+
+__attribute__((visibility("default"))) const char* k2h_amd_version(void) {
+  return "k2hash_amd 0.1 (FNV-1A BUILTIN, gfx950 HIP batch kernels)";
+}
+
+__attribute__((visibility("default"))) const char* k2h_amd_strerror(int code) {
+  static const char* names[] = {"ok", "invalid argument", "HIP runtime error", "out of memory", "no device"};
+  if (code == 0) return names[0];
+  if (g_err[0]) return g_err;
+  if (code < 0 && code >= -4) return names[-code];
+  return "unknown error";
+}
+
+__attribute__((visibility("default"))) int k2h_amd_set_variant(int v) {
+  int old = variant();
+  g_variant = v;
+  return old;
+}
+
+__attribute__((visibility("default"))) int k2h_amd_get_variant(void) { return variant(); }
+
+__attribute__((visibility("default"))) int k2h_amd_synth_bytes(void* out, uint64_t nbytes, uint64_t seed,
+                                                               uint64_t byte_off, void* stream) {
+  if (nbytes && !out) return fail(K2H_AMD_EINVAL, "out is NULL");
+  hipError_t e = k2h::launch_synth_bytes((uint8_t*)out, nbytes, seed, byte_off, (hipStream_t)stream);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "synth_bytes", e);
+}
+
+__attribute__((visibility("default"))) int k2h_amd_synth_lengths(uint32_t* lens, uint64_t n, uint64_t seed,
+                                                                 uint64_t first_key, uint32_t min_len,
+                                                                 uint32_t max_len, void* stream) {
+  if (n && !lens) return fail(K2H_AMD_EINVAL, "lens is NULL");
+  if (max_len < min_len) return fail(K2H_AMD_EINVAL, "max_len < min_len");
+  hipError_t e = k2h::launch_synth_lengths(lens, n, seed, first_key, min_len, max_len, (hipStream_t)stream);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "synth_lengths", e);
+}
+
+}  // extern "C"

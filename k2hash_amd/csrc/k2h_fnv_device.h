@@ -1,0 +1,137 @@
+// k2hash_amd -- device-side FNV-1a primitives for gfx950 (CDNA4).
+//
+// The reference hot loop (lib/k2hashfunc.cc:49-59) is, per key byte b,
+//     h ^= (uint64_t)(int64_t)(signed char)b;   // sign-extended (lib/k2hashfunc.cc:53,55)
+//     h *= 0x100000001b3;                        // 1099511628211 (lib/k2hashfunc.cc:56)
+// with h seeded by 14695981039346656037 (lib/k2hashfunc.cc:51).
+//
+// On CDNA4 the 64-bit state lives in two VGPRs (lo, hi) and, with P = 2^40 + 435,
+//     x_lo = lo ^ sext32(b)          x_hi = hi ^ sign(b)   (sign(b) = 0 or 0xffffffff)
+//     h'   = x * P = x_lo*435 + ((x_hi*435 + (x_lo << 8)) << 32)
+// which is five VALU ops per byte:
+//     v_xor_b32_sdwa  x_lo, sext(w.BYTE_k), lo
+//     v_xor_b32_sdwa  hi,   sext(u.BYTE_k), hi      u = per-byte sign smear of w (v_perm_b32)
+//     v_mul_lo_u32    m, hi, 435
+//     v_lshl_add_u32  t, x_lo, 8, m                  written into the odd half of a {0, t} pair
+//     v_mad_u64_u32   {lo,hi}, x_lo, 435, {0, t}
+// plus two ops per 4-byte word for the sign smear.  Measured on MI355X
+// (tools/valu_rates*.hip, profiles/r01_valu_rates.txt) every one of these issues in
+// ~4.2 cycles per wave64 per SIMD, so the mix is 5.5 slow-issue ops per byte.  hipcc's
+// own lowering of the byte loop spends 6.5 (it materialises x_lo << 8 and uses v_add3).
+//
+// The {0, t} pair needs two adjacent physical VGPRs with the low one held at zero, which
+// the compiler cannot be asked for through operand constraints, so the byte steps are
+// written as one asm statement per 16-byte chunk over a fixed register window (v[48:55]
+// below, declared as clobbers so the allocator keeps out).  The kernel stays under 64
+// VGPRs, i.e. 8 waves/SIMD.  A portable C++ formulation (fnv_step_c) is kept for the
+// tails and as an A/B variant.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace k2h {
+
+constexpr uint64_t kSeedBuiltin = 14695981039346656037ULL;  // lib/k2hashfunc.cc:51
+constexpr uint64_t kSeedStd = 2166136261ULL;                  // libstdc++ _Fnv_hash_impl default
+constexpr uint32_t kPrimeLo = 0x1b3u;                         // 1099511628211 = 2^40 + 0x1b3
+constexpr uint32_t kSmearSel = 0x090B080Au;                   // v_perm selector, see smear()
+
+// Per-byte sign smear: byte k of the result is 0xff if byte k of w is >= 0x80, else 0.
+// v_perm_b32 selectors 8..11 replicate the sign of bytes 1,3,5,7 of {src0:src1}; with
+// src1 = w, src0 = w << 8 those are w.b1, w.b3, w.b0, w.b2.
+__device__ __forceinline__ uint32_t smear(uint32_t w) {
+  return __builtin_amdgcn_perm(w << 8, w, kSmearSel);
+}
+
+// Portable one-byte step on the split state (compiler-scheduled).
+__device__ __forceinline__ void fnv_step_c(uint32_t& lo, uint32_t& hi, uint32_t byte) {
+  int32_t sb = (int32_t)(int8_t)byte;
+  uint32_t xlo = lo ^ (uint32_t)sb;
+  uint32_t xhi = hi ^ (uint32_t)(sb >> 31);
+  uint32_t t = xhi * kPrimeLo + (xlo << 8);
+  uint64_t r = (uint64_t)xlo * kPrimeLo + ((uint64_t)t << 32);
+  lo = (uint32_t)r;
+  hi = (uint32_t)(r >> 32);
+}
+
+__device__ __forceinline__ void fnv_word_c(uint32_t& lo, uint32_t& hi, uint32_t w) {
+  uint32_t u = smear(w);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    int32_t sb = (int32_t)(int8_t)(w >> (8 * k));
+    int32_t sm = (int32_t)(int8_t)(u >> (8 * k));
+    uint32_t xlo = lo ^ (uint32_t)sb;
+    uint32_t xhi = hi ^ (uint32_t)sm;
+    uint32_t t = xhi * kPrimeLo + (xlo << 8);
+    uint64_t r = (uint64_t)xlo * kPrimeLo + ((uint64_t)t << 32);
+    lo = (uint32_t)r;
+    hi = (uint32_t)(r >> 32);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Hand-scheduled chunk steps.  Register window (clobbered):
+//   v48 lo, v49 hi   state pair (mad64 destination)
+//   v50 = 0, v51 = t the {0, t} addend pair
+//   v52 x_lo, v53 m, v54 u (sign smear), v55 w << 8
+// ---------------------------------------------------------------------------
+#define K2H_ASM_STEP(W, K)                                                                         \
+  "v_xor_b32_sdwa v52, sext(%[" #W "]), v48 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #K \
+  " src1_sel:DWORD\n\t"                                                                            \
+  "v_xor_b32_sdwa v49, sext(v54), v49 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #K        \
+  " src1_sel:DWORD\n\t"                                                                            \
+  "v_mul_lo_u32 v53, v49, %[p]\n\t"                                                                \
+  "v_lshl_add_u32 v51, v52, 8, v53\n\t"                                                            \
+  "v_mad_u64_u32 v[48:49], vcc, v52, %[p], v[50:51]\n\t"
+
+#define K2H_ASM_SMEAR(W)                \
+  "v_lshlrev_b32 v55, 8, %[" #W "]\n\t" \
+  "v_perm_b32 v54, v55, %[" #W "], %[sel]\n\t"
+
+#define K2H_ASM_WORD(W) K2H_ASM_SMEAR(W) K2H_ASM_STEP(W, 0) K2H_ASM_STEP(W, 1) K2H_ASM_STEP(W, 2) K2H_ASM_STEP(W, 3)
+
+#define K2H_ASM_BEGIN "v_mov_b32 v48, %[lo]\n\tv_mov_b32 v49, %[hi]\n\tv_mov_b32 v50, 0\n\t"
+#define K2H_ASM_END "v_mov_b32 %[lo], v48\n\tv_mov_b32 %[hi], v49\n\t"
+#define K2H_ASM_SNAP "v_mov_b32 %[lo2], v48\n\tv_mov_b32 %[hi2], v49\n\t"
+#define K2H_ASM_CLOBBERS "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc"
+
+// 16 bytes (one uint4 chunk) into the state.
+__device__ __forceinline__ void fnv_chunk16(uint32_t& lo, uint32_t& hi, uint4 c) {
+  asm(K2H_ASM_BEGIN K2H_ASM_WORD(w0) K2H_ASM_WORD(w1) K2H_ASM_WORD(w2) K2H_ASM_WORD(w3) K2H_ASM_END
+      : [lo] "+v"(lo), [hi] "+v"(hi)
+      : [w0] "v"(c.x), [w1] "v"(c.y), [w2] "v"(c.z), [w3] "v"(c.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+      : K2H_ASM_CLOBBERS);
+}
+
+// 32 bytes (two chunks), one statement.
+__device__ __forceinline__ void fnv_chunk32(uint32_t& lo, uint32_t& hi, uint4 a, uint4 b) {
+  asm(K2H_ASM_BEGIN K2H_ASM_WORD(w0) K2H_ASM_WORD(w1) K2H_ASM_WORD(w2) K2H_ASM_WORD(w3)
+          K2H_ASM_WORD(w4) K2H_ASM_WORD(w5) K2H_ASM_WORD(w6) K2H_ASM_WORD(w7) K2H_ASM_END
+      : [lo] "+v"(lo), [hi] "+v"(hi)
+      : [w0] "v"(a.x), [w1] "v"(a.y), [w2] "v"(a.z), [w3] "v"(a.w), [w4] "v"(b.x), [w5] "v"(b.y),
+        [w6] "v"(b.z), [w7] "v"(b.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+      : K2H_ASM_CLOBBERS);
+}
+
+// Last 16-byte chunk of a key: also returns the state before the final byte
+// (the reference's second hash, lib/k2hashfunc.cc:83-85).
+__device__ __forceinline__ void fnv_chunk16_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4 c) {
+  asm(K2H_ASM_BEGIN K2H_ASM_WORD(w0) K2H_ASM_WORD(w1) K2H_ASM_WORD(w2) K2H_ASM_SMEAR(w3) K2H_ASM_STEP(w3, 0)
+          K2H_ASM_STEP(w3, 1) K2H_ASM_STEP(w3, 2) K2H_ASM_SNAP K2H_ASM_STEP(w3, 3) K2H_ASM_END
+      : [lo] "+v"(lo), [hi] "+v"(hi), [lo2] "=&v"(lo2), [hi2] "=&v"(hi2)
+      : [w0] "v"(c.x), [w1] "v"(c.y), [w2] "v"(c.z), [w3] "v"(c.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+      : K2H_ASM_CLOBBERS);
+}
+
+__device__ __forceinline__ void fnv_chunk32_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4 a,
+                                                 uint4 b) {
+  asm(K2H_ASM_BEGIN K2H_ASM_WORD(w0) K2H_ASM_WORD(w1) K2H_ASM_WORD(w2) K2H_ASM_WORD(w3) K2H_ASM_WORD(w4)
+          K2H_ASM_WORD(w5) K2H_ASM_WORD(w6) K2H_ASM_SMEAR(w7) K2H_ASM_STEP(w7, 0) K2H_ASM_STEP(w7, 1)
+              K2H_ASM_STEP(w7, 2) K2H_ASM_SNAP K2H_ASM_STEP(w7, 3) K2H_ASM_END
+      : [lo] "+v"(lo), [hi] "+v"(hi), [lo2] "=&v"(lo2), [hi2] "=&v"(hi2)
+      : [w0] "v"(a.x), [w1] "v"(a.y), [w2] "v"(a.z), [w3] "v"(a.w), [w4] "v"(b.x), [w5] "v"(b.y),
+        [w6] "v"(b.z), [w7] "v"(b.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+      : K2H_ASM_CLOBBERS);
+}
+
+}  // namespace k2h

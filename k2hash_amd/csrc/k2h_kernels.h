@@ -1,0 +1,32 @@
+// k2hash_amd -- internal launch interface between the C-ABI (k2h_batch.cc) and the
+// HIP kernels.  Not part of the public ABI (see include/k2hash_amd.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace k2h {
+
+constexpr uint64_t kSeedBuiltinValue = 14695981039346656037ULL;  // lib/k2hashfunc.cc:51
+constexpr uint64_t kSeedStdValue = 2166136261ULL;                  // libstdc++ _Fnv_hash_impl seed
+
+// Kernel variant selector (A/B measurement knob, K2H_AMD_VARIANT env / k2h_amd_set_variant).
+enum {
+  kVariantAuto = 0,      // best known kernel per shape
+  kVariantCompiler = 1,  // fixed32: compiler-scheduled byte step instead of the hand-scheduled one
+  kVariantGeneric = 2,   // fixed32: force the generic any-length kernel
+  kVariantSimpleCsr = 3, // csr: one lane per key in input order (no length balancing)
+};
+
+hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
+                        int variant, hipStream_t stream);
+hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+                      uint64_t* h2, int variant, hipStream_t stream);
+hipError_t launch_csr_simple(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+                             uint64_t* h2, hipStream_t stream);
+
+// Synthetic inputs (bench/test harness; same spec as oracle/fnv_oracle.c generators).
+hipError_t launch_synth_bytes(uint8_t* out, uint64_t nbytes, uint64_t seed, uint64_t byte_off, hipStream_t stream);
+hipError_t launch_synth_lengths(uint32_t* lens, uint64_t n, uint64_t seed, uint64_t first_key, uint32_t min_len,
+                                uint32_t max_len, hipStream_t stream);
+
+}  // namespace k2h

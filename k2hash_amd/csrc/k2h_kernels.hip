@@ -1,0 +1,205 @@
+// k2hash_amd -- batched FNV-1a key-hash kernels for MI355X (gfx950).
+//
+// Bit-exact restatement of lib/k2hashfunc.cc:49-91 (k2h_Fnv_hash / k2h_hash /
+// k2h_second_hash) over millions of independent keys per launch.  FNV-1a is a
+// strictly serial chain per key, so one lane owns one key; a wave hashes 64 keys
+// side by side.  Both hashes come from one pass: the reference's second hash is the
+// FNV state after length-1 bytes (lib/k2hashfunc.cc:83-85), i.e. the state just
+// before the final byte.
+//
+// Kernels:
+//   fixed32      16M x 32-byte keys (BASELINE config 2).  Each lane loads its key
+//                with two 16-byte loads; a wave reads one contiguous 2 KiB run.
+//   fixed        any key length, any alignment; per-lane unaligned 16-byte loads.
+//   csr          offsets+bytes (CSR) keys of any length (configs 3, 5); see k2h_csr.hip.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "k2h_fnv_device.h"
+#include "k2h_kernels.h"
+
+namespace k2h {
+
+typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
+
+__device__ __forceinline__ uint4 load16_ua(const uint8_t* p) {
+  u32x4_ua v = *reinterpret_cast<const u32x4_ua*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// Load up to 16 bytes at p without touching memory at or beyond `end` (bytes past
+// the key are don't-care; the caller masks them by length).
+__device__ __forceinline__ uint4 load16_guarded(const uint8_t* p, const uint8_t* end) {
+  if (p + 16 <= end) return load16_ua(p);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (int j = 0; j < 16 && p + j < end; ++j) w[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Hash the final 1..16 bytes of a key held in c (byte 0 first); returns h1 in (lo,hi)
+// and the state before the last byte in (lo2,hi2).
+__device__ __forceinline__ void fnv_tail(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4 c,
+                                         uint32_t r) {
+  uint64_t q0 = ((uint64_t)c.y << 32) | c.x, q1 = ((uint64_t)c.w << 32) | c.z;
+  for (uint32_t j = 0; j < r; ++j) {
+    if (j + 1 == r) {
+      lo2 = lo;
+      hi2 = hi;
+    }
+    fnv_step_c(lo, hi, (uint32_t)q0 & 0xffu);
+    q0 = (q0 >> 8) | (q1 << 56);
+    q1 >>= 8;
+  }
+}
+
+__device__ __forceinline__ uint64_t pack(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+// ---------------------------------------------------------------------------
+// fixed32: key i = keys[32*i .. 32*i+32), keys 16-byte aligned.
+// ---------------------------------------------------------------------------
+template <bool H2, bool ASM>
+__global__ __launch_bounds__(256) void fnv_fixed32_kernel(const uint4* __restrict__ keys, uint64_t n, uint64_t seed,
+                                                          uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  uint4 a = keys[2 * i], b = keys[2 * i + 1];
+  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2, hi2;
+  if constexpr (ASM) {
+    if constexpr (H2) {
+      fnv_chunk32_last(lo, hi, lo2, hi2, a, b);
+    } else {
+      fnv_chunk32(lo, hi, a, b);
+    }
+  } else {
+    uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int j = 0; j < 7; ++j) fnv_word_c(lo, hi, w[j]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (k == 3) {
+        lo2 = lo;
+        hi2 = hi;
+      }
+      fnv_step_c(lo, hi, (w[7] >> (8 * k)) & 0xffu);
+    }
+  }
+  h1[i] = pack(lo, hi);
+  if constexpr (H2) h2[i] = pack(lo2, hi2);
+}
+
+// ---------------------------------------------------------------------------
+// fixed: key i = base[L*i .. L*i+L), any L >= 1, any alignment.  The loop trip
+// count is wave-uniform (L is a kernel argument), so no lane diverges.
+// ---------------------------------------------------------------------------
+template <bool H2>
+__global__ __launch_bounds__(256) void fnv_fixed_kernel(const uint8_t* __restrict__ base, uint64_t key_len, uint64_t n,
+                                                        uint64_t seed, uint64_t* __restrict__ h1,
+                                                        uint64_t* __restrict__ h2) {
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* p = base + key_len * i;
+  const uint8_t* end = base + key_len * n;
+  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2 = lo, hi2 = hi;
+  uint64_t nfull = (key_len - 1) / 16;  // chunks strictly before the one holding the last byte
+  for (uint64_t c = 0; c < nfull; ++c) fnv_chunk16(lo, hi, load16_ua(p + 16 * c));
+  uint32_t r = (uint32_t)(key_len - 16 * nfull);
+  fnv_tail(lo, hi, lo2, hi2, load16_guarded(p + 16 * nfull, end), r);
+  if (key_len == 1) {  // length 1: the second hash is not shortened (lib/k2hashfunc.cc:83)
+    lo2 = lo;
+    hi2 = hi;
+  }
+  h1[i] = pack(lo, hi);
+  if constexpr (H2) h2[i] = pack(lo2, hi2);
+}
+
+// ---------------------------------------------------------------------------
+// zero fill (length-0 keys, NULL key buffers: lib/k2hashfunc.cc:66-68)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void fill_zero_kernel(uint64_t* __restrict__ p, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i < n) p[i] = 0;
+}
+
+static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
+                        int variant, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (!keys || key_len == 0) {
+    fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n);
+    if (h2) fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h2, n);
+    return hipGetLastError();
+  }
+  bool aligned16 = ((uintptr_t)keys & 15u) == 0;
+  if (key_len == 32 && aligned16 && variant != kVariantGeneric) {
+    const uint4* k = (const uint4*)keys;
+    bool use_asm = variant != kVariantCompiler;
+    if (h2) {
+      if (use_asm) fnv_fixed32_kernel<true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
+      else fnv_fixed32_kernel<true, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
+    } else {
+      if (use_asm) fnv_fixed32_kernel<false, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
+      else fnv_fixed32_kernel<false, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
+    }
+    return hipGetLastError();
+  }
+  if (h2) fnv_fixed_kernel<true><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)keys, key_len, n, seed, h1, h2);
+  else fnv_fixed_kernel<false><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)keys, key_len, n, seed, h1, nullptr);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// csr v0: one lane per key in input order (no length balancing).
+// ---------------------------------------------------------------------------
+template <bool H2>
+__global__ __launch_bounds__(256) void fnv_csr_simple_kernel(const uint8_t* __restrict__ bytes,
+                                                             const uint64_t* __restrict__ offsets, uint64_t n,
+                                                             uint64_t seed, uint64_t* __restrict__ h1,
+                                                             uint64_t* __restrict__ h2) {
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  uint64_t s = offsets[i], e = offsets[i + 1];
+  uint64_t len = e - s;
+  if (len == 0) {
+    h1[i] = 0;
+    if constexpr (H2) h2[i] = 0;
+    return;
+  }
+  const uint8_t* p = bytes + s;
+  const uint8_t* end = bytes + offsets[n];
+  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2 = lo, hi2 = hi;
+  uint64_t nfull = (len - 1) / 16;
+  for (uint64_t c = 0; c < nfull; ++c) fnv_chunk16(lo, hi, load16_ua(p + 16 * c));
+  uint32_t r = (uint32_t)(len - 16 * nfull);
+  fnv_tail(lo, hi, lo2, hi2, load16_guarded(p + 16 * nfull, end), r);
+  if (len == 1) {  // length 1: the second hash is not shortened (lib/k2hashfunc.cc:83)
+    lo2 = lo;
+    hi2 = hi;
+  }
+  h1[i] = pack(lo, hi);
+  if constexpr (H2) h2[i] = pack(lo2, hi2);
+}
+
+hipError_t launch_csr_simple(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+                             uint64_t* h2, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (!bytes) {
+    fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n);
+    if (h2) fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h2, n);
+    return hipGetLastError();
+  }
+  if (h2)
+    fnv_csr_simple_kernel<true><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)bytes, offsets, n, seed, h1, h2);
+  else
+    fnv_csr_simple_kernel<false><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)bytes, offsets, n, seed, h1,
+                                                                    nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+                      uint64_t* h2, int variant, hipStream_t stream) {
+  (void)variant;
+  return launch_csr_simple(bytes, offsets, n, seed, h1, h2, stream);
+}
+
+}  // namespace k2h

@@ -1,0 +1,94 @@
+"""Multi-GPU partitioning of a key batch and the gather of its hashes.
+
+Keys are independent (lib/k2hashfunc.cc:49-59 has no cross-key state), so the
+batch shards with no data-path collective: rank r hashes a contiguous key range.
+The only exchange is returning the 64-bit hashes to whoever indexes the k2hash
+table -- an RCCL gather over xGMI (torch.distributed "nccl" backend = RCCL on
+ROCm), or all-gather when every rank needs every hash.  The same code runs over
+gloo on CPU tensors for tests.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+
+
+def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous, balanced key range [first, last) of rank `rank` (equal counts +-1)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    q, r = divmod(n, world)
+    first = rank * q + min(rank, r)
+    return first, first + q + (1 if rank < r else 0)
+
+
+def shard_csr_by_bytes(offsets: np.ndarray, rank: int, world: int) -> tuple[int, int]:
+    """Key range [first, last) of rank `rank` such that every rank gets about the same
+    number of key BYTES (CSR keys differ in length).  Cuts fall on key boundaries."""
+    offsets = np.asarray(offsets)
+    n = offsets.size - 1
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    lo, hi = int(offsets[0]), int(offsets[-1])
+
+    def cut(k: int) -> int:
+        if k <= 0:
+            return 0
+        if k >= world:
+            return n
+        target = lo + (hi - lo) * k // world
+        return int(np.searchsorted(offsets[:-1], target, side="left"))
+
+    return cut(rank), cut(rank + 1)
+
+
+def rebase_offsets(offsets, first: int, last: int):
+    """Offsets of keys [first, last) relative to their first byte (n_local + 1 entries)."""
+    sub = offsets[first:last + 1]
+    return sub - sub[0]
+
+
+def gather_hashes(h, dst: int = 0, group=None, counts: Optional[list] = None):
+    """Gather every rank's hash vector to rank `dst` in rank (= key) order.
+
+    `h` is this rank's int64 tensor; `counts` (per-rank lengths) defaults to equal
+    lengths.  Returns the concatenated tensor on dst, None elsewhere.  Implemented as
+    point-to-point sends to the root (RCCL has no native gather; each peer uses its own
+    xGMI link to the root), posted together so they overlap.
+    """
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    if counts is None:
+        counts = [h.numel()] * world
+    if rank == dst:
+        out = torch.empty(sum(counts), dtype=h.dtype, device=h.device)
+        pieces = list(torch.split(out, counts))
+        ops = []
+        for r in range(world):
+            if r == dst:
+                pieces[r].copy_(h)
+            else:
+                ops.append(dist.P2POp(dist.irecv, pieces[r], r, group))
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        return out
+    reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, h.contiguous(), dst, group)])
+    for req in reqs:
+        req.wait()
+    return None
+
+
+def all_gather_hashes(h, group=None):
+    """Every rank receives all hashes (equal shard sizes), via all_gather_into_tensor."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    out = torch.empty(h.numel() * world, dtype=h.dtype, device=h.device)
+    dist.all_gather_into_tensor(out, h.contiguous(), group=group)
+    return out

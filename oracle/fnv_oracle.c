@@ -1,0 +1,136 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C restatement of yahoojapan/k2hash's key-hash path, used as the parity
+ * checker for the HIP kernels and as the CPU baseline ("port") in bench.py.
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * this file's library; the product (k2hash_amd/) never links or calls it.
+ *
+ * Pinned: every function below is checked against (a) the reference itself,
+ * compiled from /root/reference/lib/k2hashfunc.cc by oracle/Makefile into
+ * oracle/_ref/ (tests/test_oracle.py), and (b) the committed golden vectors in
+ * tests/golden/ generated from that build by oracle/gen_golden.c.
+ *
+ * Reference citations (paths relative to the reference root):
+ *   seed 14695981039346656037, prime 1099511628211 ... lib/k2hashfunc.cc:51,56
+ *   bytes read through `const char*` (signed on x86-64),
+ *   XORed as a sign-extended 64-bit value ............. lib/k2hashfunc.cc:53,55
+ *   NULL / length 0 -> 0 ................................ lib/k2hashfunc.cc:66-68, 80-82
+ *   second hash = FNV over length-1 bytes if length>1 .. lib/k2hashfunc.cc:83-85
+ *   version strings ..................................... lib/k2hashfunc.cc:35-39
+ *   USE_STD_FNV_HASH_FUNCTION variant: libstdc++ _Fnv_hash_impl::hash, seed
+ *   2166136261 (GCC 11 bits/functional_hash.h:212-217), same signed-char loop
+ *   (libstdc++ _Fnv_hash_bytes) ......................... lib/k2hashfunc.cc:69-70, 86-87
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+#define ORACLE_FNV_SEED_BUILTIN 14695981039346656037ULL
+#define ORACLE_FNV_SEED_STD 2166136261ULL
+#define ORACLE_FNV_PRIME 1099511628211ULL
+
+/* variant 0 = "FNV-1A BUILTIN" (default build), 1 = "STD::FNV BUILTIN" */
+static uint64_t seed_of(int variant) {
+  return variant ? ORACLE_FNV_SEED_STD : ORACLE_FNV_SEED_BUILTIN;
+}
+
+/* lib/k2hashfunc.cc:49-59: byte-serial xor/multiply over signed chars. */
+uint64_t oracle_fnv(const void* ptr, size_t len, uint64_t seed) {
+  const signed char* p = (const signed char*)ptr;
+  uint64_t h = seed;
+  for (size_t i = 0; i < len; ++i) {
+    h ^= (uint64_t)(int64_t)p[i];
+    h *= ORACLE_FNV_PRIME;
+  }
+  return h;
+}
+
+/* lib/k2hashfunc.cc:62-74 */
+uint64_t oracle_k2h_hash(const void* ptr, size_t length, int variant) {
+  if (!ptr || length < 1) return 0;
+  return oracle_fnv(ptr, length, seed_of(variant));
+}
+
+/* lib/k2hashfunc.cc:76-91 */
+uint64_t oracle_k2h_second_hash(const void* ptr, size_t length, int variant) {
+  if (!ptr || length < 1) return 0;
+  if (length > 1) length--;
+  return oracle_fnv(ptr, length, seed_of(variant));
+}
+
+/* lib/k2hashfunc.cc:35-39, 93-96 */
+const char* oracle_k2h_hash_version(int variant) {
+  return variant ? "STD::FNV BUILTIN" : "FNV-1A BUILTIN";
+}
+
+/* Batch forms used as checkers: CSR (key i = bytes[offsets[i] .. offsets[i+1]))
+ * and fixed-length (key i = bytes[i*key_len .. (i+1)*key_len)).  h2 may be NULL. */
+void oracle_hash_csr(const uint8_t* bytes, const uint64_t* offsets, size_t n,
+                     uint64_t* h1, uint64_t* h2, int variant) {
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t* k = bytes + offsets[i];
+    size_t len = (size_t)(offsets[i + 1] - offsets[i]);
+    h1[i] = oracle_k2h_hash(k, len, variant);
+    if (h2) h2[i] = oracle_k2h_second_hash(k, len, variant);
+  }
+}
+
+void oracle_hash_fixed(const uint8_t* bytes, size_t key_len, size_t n,
+                       uint64_t* h1, uint64_t* h2, int variant) {
+  for (size_t i = 0; i < n; ++i) {
+    const uint8_t* k = bytes + i * key_len;
+    h1[i] = oracle_k2h_hash(k, key_len, variant);
+    if (h2) h2[i] = oracle_k2h_second_hash(k, key_len, variant);
+  }
+}
+
+/* ------------------------------------------------------------------------
+ * Synthetic-input generator (spec shared with the device generator in
+ * k2hash_amd/csrc/k2h_synth.hip; independent implementation, cross-checked
+ * by tests).  splitmix64 in counter form: word j of a stream with seed s is
+ * mix(s + (j+1) * GAMMA), i.e. the j-th output of splitmix64 seeded with s.
+ * ------------------------------------------------------------------------ */
+#define GAMMA 0x9E3779B97F4A7C15ULL
+
+uint64_t oracle_splitmix_word(uint64_t seed, uint64_t j) {
+  uint64_t z = seed + (j + 1) * GAMMA;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+/* Bytes [byte_off, byte_off+nbytes) of the little-endian word stream. */
+void oracle_gen_bytes(uint64_t seed, uint64_t byte_off, size_t nbytes, uint8_t* out) {
+  size_t i = 0;
+  while (i < nbytes) {
+    uint64_t pos = byte_off + i;
+    uint64_t w = oracle_splitmix_word(seed, pos >> 3);
+    for (unsigned sh = (unsigned)(pos & 7); sh < 8 && i < nbytes; ++sh) out[i++] = (uint8_t)(w >> (8 * sh));
+  }
+}
+
+/* CSR lengths: len_i = min_len + mix(seed, i) % (max_len - min_len + 1);
+ * offsets[0] = 0, offsets[i+1] = offsets[i] + len_i. */
+void oracle_gen_offsets(uint64_t seed, uint64_t first_key, size_t n, uint32_t min_len,
+                        uint32_t max_len, uint64_t base, uint64_t* offsets) {
+  uint64_t span = (uint64_t)(max_len - min_len) + 1;
+  offsets[0] = base;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t len = min_len + oracle_splitmix_word(seed, first_key + i) % span;
+    offsets[i + 1] = offsets[i] + len;
+  }
+}
+
+/* Order-sensitive digest of a hash vector: {xor, wrapping sum, sum of h*(2i+1)}. */
+void oracle_digest(const uint64_t* h, size_t n, uint64_t first_index, uint64_t out[3]) {
+  uint64_t x = 0, s = 0, w = 0;
+  for (size_t i = 0; i < n; ++i) {
+    x ^= h[i];
+    s += h[i];
+    w += h[i] * (2 * (first_index + i) + 1);
+  }
+  out[0] = x;
+  out[1] = s;
+  out[2] = w;
+}

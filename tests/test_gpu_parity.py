@@ -1,0 +1,223 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the oracle and the
+golden fixtures generated from the reference build.  Bit-exact (integer path).
+
+Sizes: seeded inputs the oracle finishes in seconds are compared hash for hash;
+BASELINE.json's full sizes (configs 2, 3, 5 and the 8-shard config 4) are compared
+through order-sensitive digests (tests/golden/digests.json, computed from the
+reference itself over the same synthetic inputs).
+"""
+import numpy as np
+import pytest
+
+from conftest import hexkey, u64
+
+import k2hash_amd
+from k2hash_amd import batch
+
+pytestmark = pytest.mark.gpu
+
+VARIANTS = [0, 1, 2, 3]
+
+
+def dev_u8(torch, arr, device, pad_front=0):
+    """Device copy of a host byte array, optionally starting `pad_front` bytes into
+    the allocation (to exercise unaligned key buffers)."""
+    t = torch.zeros(arr.size + pad_front + 16, dtype=torch.uint8, device=device)
+    t[pad_front:pad_front + arr.size] = torch.from_numpy(np.ascontiguousarray(arr))
+    return t[pad_front:pad_front + arr.size]
+
+
+def host_u64(t):
+    return t.cpu().numpy().view(np.uint64)
+
+
+@pytest.fixture(autouse=True)
+def _reset_variant():
+    yield
+    batch.set_variant(0)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 257, 4099, 100003])
+def test_fixed32_vs_oracle(cuda, oracle, n, variant):
+    import torch
+    batch.set_variant(variant)
+    data = oracle.gen_bytes(32 * n, byte_off=32 * 12345)
+    r1, r2 = oracle.hash_fixed(data, 32)
+    keys = dev_u8(torch, data, cuda)
+    h1, h2 = k2hash_amd.hash_fixed(keys, 32, second=True)
+    g1, _ = k2hash_amd.hash_fixed(keys, 32, second=False)
+    torch.cuda.synchronize()
+    assert np.array_equal(host_u64(h1), r1)
+    assert np.array_equal(host_u64(h2), r2)
+    assert np.array_equal(host_u64(g1), r1)
+
+
+@pytest.mark.parametrize("key_len", list(range(1, 72)) + [95, 96, 97, 127, 128, 129, 255, 256, 257, 1000, 4095, 4096])
+def test_fixed_any_length_vs_oracle(cuda, oracle, key_len):
+    import torch
+    n = 517 if key_len < 1000 else 67
+    data = oracle.gen_bytes(key_len * n, byte_off=7 * key_len)
+    r1, r2 = oracle.hash_fixed(data, key_len)
+    for pad in (0, 1, 6):
+        keys = dev_u8(torch, data, cuda, pad_front=pad)
+        h1, h2 = k2hash_amd.hash_fixed(keys, key_len, second=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(host_u64(h1), r1), (key_len, pad)
+        assert np.array_equal(host_u64(h2), r2), (key_len, pad)
+
+
+def _csr(keys):
+    data = np.frombuffer(b"".join(keys), np.uint8) if keys else np.zeros(0, np.uint8)
+    off = np.zeros(len(keys) + 1, np.int64)
+    off[1:] = np.cumsum([len(k) for k in keys])
+    return data, off
+
+
+@pytest.mark.parametrize("variant", [0, 3])
+def test_golden_vectors_csr(cuda, vectors, variant):
+    import torch
+    batch.set_variant(variant)
+    for field, std in (("vectors", False), ("std_fnv_vectors", True)):
+        vs = vectors[field]
+        data, off = _csr([hexkey(v) for v in vs])
+        d = torch.from_numpy(data.copy()).to(cuda) if data.size else torch.zeros(0, dtype=torch.uint8, device=cuda)
+        h1, h2 = k2hash_amd.hash_csr(d, torch.from_numpy(off).to(cuda), second=True, std_fnv=std)
+        torch.cuda.synchronize()
+        a, b = host_u64(h1), host_u64(h2)
+        for i, v in enumerate(vs):
+            assert (int(a[i]), int(b[i])) == (u64(v["h1"]), u64(v["h2"])), (field, v["tag"], v["len"])
+
+
+@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("lens", ["mixed", "zeros", "long", "uniform"])
+def test_csr_vs_oracle(cuda, oracle, lens, variant):
+    import torch
+    batch.set_variant(variant)
+    rng = np.random.default_rng(5)
+    if lens == "mixed":
+        L = rng.integers(0, 300, 6000)
+        L[rng.integers(0, 6000, 300)] = 0
+    elif lens == "zeros":
+        L = np.zeros(1000, np.int64)
+        L[::7] = 1
+    elif lens == "long":
+        L = rng.integers(1000, 9000, 300)
+    else:
+        L = rng.integers(8, 257, 20000)
+    off = np.zeros(L.size + 1, np.int64)
+    off[1:] = np.cumsum(L)
+    base = 3  # offsets need not start at 0
+    off += base
+    data = oracle.gen_bytes(int(off[-1]) + 5)
+    r1, r2 = oracle.hash_csr(data, off.astype(np.uint64))
+    d = dev_u8(torch, data, cuda, pad_front=1)
+    h1, h2 = k2hash_amd.hash_csr(d, torch.from_numpy(off).to(cuda), second=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(host_u64(h1), r1)
+    assert np.array_equal(host_u64(h2), r2)
+
+
+def test_std_fnv_flag(cuda, oracle):
+    import torch
+    data = oracle.gen_bytes(32 * 1000)
+    r1, r2 = oracle.hash_fixed(data, 32, variant=1)
+    h1, h2 = k2hash_amd.hash_fixed(dev_u8(torch, data, cuda), 32, second=True, std_fnv=True)
+    torch.cuda.synchronize()
+    assert np.array_equal(host_u64(h1), r1) and np.array_equal(host_u64(h2), r2)
+
+
+def test_empty_and_null(cuda):
+    import torch
+    off = torch.tensor([0, 0, 0, 0], dtype=torch.int64, device=cuda)
+    h1, h2 = k2hash_amd.hash_csr(torch.zeros(0, dtype=torch.uint8, device=cuda), off, second=True)
+    torch.cuda.synchronize()
+    assert not h1.any() and not h2.any()
+    h1, _ = k2hash_amd.hash_csr(torch.zeros(4, dtype=torch.uint8, device=cuda),
+                                torch.zeros(1, dtype=torch.int64, device=cuda))
+    assert h1.numel() == 0
+
+
+def test_non_default_stream(cuda, oracle):
+    import torch
+    data = oracle.gen_bytes(32 * 5000)
+    r1, _ = oracle.hash_fixed(data, 32)
+    keys = dev_u8(torch, data, cuda)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        h1, _ = k2hash_amd.hash_fixed(keys, 32)
+    s.synchronize()
+    assert np.array_equal(host_u64(h1), r1)
+
+
+def test_synth_matches_oracle_generator(cuda, oracle):
+    import torch
+    for nbytes, off in ((1, 0), (37, 5), (4096, 3), (100000, 8 * 1000 + 1)):
+        t = batch.synth_bytes(nbytes, cuda, byte_off=off)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), oracle.gen_bytes(nbytes, byte_off=off)), (nbytes, off)
+    o = batch.synth_offsets(5000, cuda, first_key=77)
+    assert np.array_equal(o.cpu().numpy().astype(np.uint64), oracle.gen_offsets(5000, first_key=77))
+
+
+def test_host_api_vs_oracle(cuda, oracle):
+    n = (1 << 21) + 12345  # spans two 64 MiB pipeline chunks at 32 B
+    data = oracle.gen_bytes(32 * n)
+    r1, r2 = oracle.hash_fixed(data, 32)
+    h1, h2 = k2hash_amd.hash_fixed_host(data, 32, second=True)
+    assert np.array_equal(h1, r1) and np.array_equal(h2, r2)
+    h1, _ = k2hash_amd.hash_fixed_host(data[: 21 * 1000], 21)
+    assert np.array_equal(h1, oracle.hash_fixed(data[: 21 * 1000], 21)[0])
+    off = oracle.gen_offsets(400000)
+    cdata = oracle.gen_bytes(int(off[-1]))
+    c1, c2 = oracle.hash_csr(cdata, off)
+    g1, g2 = k2hash_amd.hash_csr_host(cdata, off, second=True)
+    assert np.array_equal(g1, c1) and np.array_equal(g2, c2)
+
+
+# ---------------------------------------------------------------------------------------
+# Full BASELINE sizes, checked through digests of the reference's own outputs.
+# ---------------------------------------------------------------------------------------
+def _check_digest(oracle, cfg, h1, h2, first=0, expect=None):
+    d1 = oracle.digest(host_u64(h1), first)
+    d2 = oracle.digest(host_u64(h2), first)
+    exp = expect or cfg
+    assert [f"{x:016x}" for x in d1] == exp["h1"]
+    assert [f"{x:016x}" for x in d2] == exp["h2"]
+
+
+@pytest.mark.parametrize("name", ["fixed32_16M", "fixed4096_1M", "fixed21_1M", "fixed32_64K"])
+def test_full_size_fixed_digest(cuda, oracle, digests, name):
+    import torch
+    cfg = digests[name]
+    keys = batch.synth_bytes(cfg["n"] * cfg["key_len"], cuda)
+    h1, h2 = k2hash_amd.hash_fixed(keys, cfg["key_len"], second=True)
+    torch.cuda.synchronize()
+    _check_digest(oracle, cfg, h1, h2)
+    g1, _ = k2hash_amd.hash_fixed(keys, cfg["key_len"])  # h1-only path (the bench path)
+    torch.cuda.synchronize()
+    assert torch.equal(g1, h1)
+
+
+@pytest.mark.parametrize("name", ["csr_8_256_64M", "csr_8_256_64K"])
+def test_full_size_csr_digest(cuda, oracle, digests, name):
+    import torch
+    cfg = digests[name]
+    off = batch.synth_offsets(cfg["n"], cuda, cfg["min_len"], cfg["max_len"])
+    data = batch.synth_bytes(int(off[-1].item()), cuda)
+    h1, h2 = k2hash_amd.hash_csr(data, off, second=True)
+    torch.cuda.synchronize()
+    _check_digest(oracle, cfg, h1, h2)
+
+
+def test_config4_shard_digests(cuda, oracle, digests):
+    """Config 4 (1 B x 32 B over 8 GPUs): each rank's shard, hashed here one at a time,
+    matches the reference's digest of that shard."""
+    import torch
+    cfg = digests["fixed32_1G"]
+    for c in cfg["chunks"][:2]:
+        keys = batch.synth_bytes(c["count"] * 32, cuda, byte_off=c["first"] * 32)
+        h1, h2 = k2hash_amd.hash_fixed(keys, 32, second=True)
+        torch.cuda.synchronize()
+        _check_digest(oracle, cfg, h1, h2, first=c["first"], expect=c)
+        del keys, h1, h2

@@ -1,0 +1,165 @@
+"""Drop-in boundary (include/k2hash_amd.h section 1) and C-ABI surface, on CPU.
+
+The plugin must satisfy K2HashDynLib::Load (lib/k2hashfunc.cc:132-161): dlopen
+RTLD_LAZY, dlsym of k2h_hash / k2h_second_hash / k2h_hash_version, all-or-nothing,
+and return the reference's hashes bit for bit.
+"""
+import ctypes
+import ctypes.util
+import os
+import re
+import subprocess
+import threading
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, hexkey, u64
+
+import k2hash_amd
+from k2hash_amd import _native
+from k2hash_amd.hashfunc import K2HashDynLib, K2H_2ND_HASH_FUNC, K2H_HASH_FUNC, K2H_HASH_VER_FUNC
+
+PLUGINS = [_native.PLUGIN_LIB, _native.BATCH_LIB]
+
+
+def header_symbols():
+    text = (ROOT / "include" / "k2hash_amd.h").read_text()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b((?:k2h|k2h_amd)_\w+)\s*\(", text)))
+
+
+def test_header_symbols_exported():
+    syms = header_symbols()
+    assert "k2h_hash" in syms and "k2h_amd_hash_csr" in syms
+    lib = ctypes.CDLL(str(_native.BATCH_LIB))
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_native.SIGNATURES), "binding table out of sync with the header"
+    plug = ctypes.CDLL(str(_native.PLUGIN_LIB))
+    for s in _native.PLUGIN_SYMBOLS:
+        assert hasattr(plug, s)
+
+
+def test_plugin_has_no_hip_dependency():
+    out = subprocess.run(["ldd", str(_native.PLUGIN_LIB)], capture_output=True, text=True).stdout
+    assert "amdhip" not in out and "hsa" not in out
+
+
+@pytest.mark.parametrize("so", PLUGINS, ids=lambda p: p.name)
+def test_plugin_vectors(so, vectors):
+    lib = _native.plugin_lib(so)
+    assert lib.k2h_hash_version() == b"FNV-1A BUILTIN"  # lib/k2hashfunc.cc:38
+    for v in vectors["vectors"]:
+        k = hexkey(v)
+        assert lib.k2h_hash(k, len(k)) == u64(v["h1"]), v["tag"]
+        assert lib.k2h_second_hash(k, len(k)) == u64(v["h2"]), v["tag"]
+
+
+def test_null_and_zero_length():
+    lib = _native.plugin_lib()
+    # lib/k2hashfunc.cc:66-68, 80-82
+    assert lib.k2h_hash(None, 10) == 0 and lib.k2h_second_hash(None, 10) == 0
+    assert lib.k2h_hash(b"abc", 0) == 0 and lib.k2h_second_hash(b"abc", 0) == 0
+    assert lib.k2h_hash(b"a", 1) == lib.k2h_second_hash(b"a", 1)  # length 1: h2 == h1
+
+
+def test_dynlib_mirror_load_and_dispatch(vectors):
+    dl = K2HashDynLib.get()
+    assert dl.Load(_native.PLUGIN_LIB)
+    try:
+        assert K2H_HASH_VER_FUNC() == "FNV-1A BUILTIN"
+        # tests/k2hexttest.cc:166-175 prints these for "0123456789" (strlen, no NUL)
+        assert K2H_HASH_FUNC(b"0123456789") == 0x50c0aafd8b4330b2
+        assert K2H_2ND_HASH_FUNC(b"0123456789") == 0xa947a7387dabffbf
+    finally:
+        dl.Unload()
+    assert not dl.Load("/nonexistent/libnothing.so")
+    # a library missing one of the three symbols is rejected, all-or-nothing
+    assert not dl.Load(ctypes.util.find_library("m") or "libm.so.6")
+    assert dl.get_k2h_hash() is None
+
+
+def test_reference_loader_accepts_plugin(oracle, vectors, tmp_path):
+    """The reference's own K2HashDynLib::Load + K2H_HASH_FUNC macros over our plugin."""
+    if not oracle.REF_CONFORMANCE.exists() and not oracle.build_ref():
+        pytest.skip("reference build unavailable")
+    keys = [v for v in vectors["vectors"] if v["len"] <= 4096][:400]
+    inp = "\n".join(v["key"] or "-" for v in keys) + "\n"
+    for so in PLUGINS:
+        r = subprocess.run([str(oracle.REF_CONFORMANCE), str(so)], input=inp, capture_output=True, text=True,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        lines = r.stdout.splitlines()
+        assert lines[0] == "LOAD ok"
+        assert lines[1] == "VERSION FNV-1A BUILTIN"
+        assert lines[2] == "BUILTIN FNV-1A BUILTIN"
+        got = lines[3:]
+        assert len(got) == len(keys)
+        for v, line in zip(keys, got):
+            a, b = line.split()
+            assert (u64(a), u64(b)) == (u64(v["h1"]), u64(v["h2"])), v["tag"]
+
+
+def test_reference_loader_with_reference_sample_plugin(oracle):
+    """Sanity of the conformance driver itself: the reference's sample DSO
+    (tests/k2htesthashfunc.cc) loads and reports its own version string."""
+    if not oracle.REF_CONFORMANCE.exists() and not oracle.build_ref():
+        pytest.skip("reference build unavailable")
+    r = subprocess.run([str(oracle.REF_CONFORMANCE), str(oracle.REF_TESTHASH_SO)], input="6162\n",
+                       capture_output=True, text=True, timeout=60)
+    assert r.stdout.splitlines()[:2] == ["LOAD ok", "VERSION DSO HASH V1.0"]
+    assert r.stdout.splitlines()[3] == "0000000000006162 0000000000006261"
+
+
+def test_scalar_threads_and_fork(vectors):
+    lib = _native.plugin_lib()
+    keys = [(hexkey(v), u64(v["h1"]), u64(v["h2"])) for v in vectors["vectors"]]
+    errors = []
+
+    def worker():
+        for k, a, b in keys:
+            if lib.k2h_hash(k, len(k)) != a or lib.k2h_second_hash(k, len(k)) != b:
+                errors.append(k)
+
+    th = [threading.Thread(target=worker) for _ in range(8)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors
+    pid = os.fork()  # k2hbench forks after initialisation (tests/k2hbench.cc:1170)
+    if pid == 0:
+        ok = all(lib.k2h_hash(k, len(k)) == a for k, a, _ in keys)
+        os._exit(0 if ok else 1)
+    _, status = os.waitpid(pid, 0)
+    assert os.WEXITSTATUS(status) == 0
+
+
+def test_batch_abi_argument_errors():
+    lib = _native.batch_lib()
+    assert lib.k2h_amd_hash_fixed(None, 32, 0, None, None, 0, None) == _native.K2H_AMD_OK  # n == 0
+    assert lib.k2h_amd_hash_fixed(None, 32, 10, None, None, 0, None) == _native.K2H_AMD_EINVAL
+    assert lib.k2h_amd_hash_csr(None, None, 10, ctypes.c_void_p(8), None, 0, None) == _native.K2H_AMD_EINVAL
+    assert lib.k2h_amd_hash_fixed(ctypes.c_void_p(16), 1 << 40, 1 << 40, ctypes.c_void_p(8), None, 0,
+                                  None) == _native.K2H_AMD_EINVAL  # overflow
+    assert b"h1" in lib.k2h_amd_strerror(_native.K2H_AMD_EINVAL) or lib.k2h_amd_strerror(-1)
+    assert lib.k2h_amd_version().startswith(b"k2hash_amd")
+
+
+def test_host_api_null_buffers_without_gpu():
+    # NULL key buffer -> every hash 0 (lib/k2hashfunc.cc:66-68); needs no device
+    h1 = np.full(5, 7, np.uint64)
+    h2 = np.full(5, 7, np.uint64)
+    lib = _native.batch_lib()
+    rc = lib.k2h_amd_hash_fixed_host(None, 32, 5, ctypes.c_void_p(h1.ctypes.data),
+                                     ctypes.c_void_p(h2.ctypes.data), 0, 0)
+    assert rc == 0 and not h1.any() and not h2.any()
+
+
+def test_python_mirror_scalar():
+    assert k2hash_amd.k2h_hash(b"KEY-0000000000000000\0") == 0x0b2bb3288cdb4d49
+    assert k2hash_amd.k2h_second_hash(b"KEY-0000000000000000\0") == 0x1bfb06d77c7f9f13
+    assert k2hash_amd.k2h_hash(None) == 0 and k2hash_amd.k2h_hash(b"") == 0
+    assert k2hash_amd.k2h_hash_version() == "FNV-1A BUILTIN"
