@@ -1,0 +1,436 @@
+// k2hash_amd -- kernels for variable-length (CSR) keys and long fixed-length keys.
+//
+// FNV-1a (lib/k2hashfunc.cc:49-59) is serial per key, so one lane owns one key and a
+// wave runs as long as its longest key.  Three measures keep a wave's 64 lanes busy
+// and its memory traffic line-efficient:
+//
+//  1. End-aligned 16-byte chunks.  A key of len bytes is hashed as k = ceil(len/16)
+//     whole chunks ending exactly at its last byte; the first chunk starts p = 16k-len
+//     bytes early and its p leading bytes are zeroed.  A zero byte is a pure multiply
+//     (h ^= 0; h *= P), so starting from S_p = seed * P^-p (mod 2^64) those p steps
+//     land exactly on the seed.  Every lane therefore runs whole hand-scheduled chunk
+//     steps with no per-byte tail loop, and the second hash -- the state before the
+//     final byte (lib/k2hashfunc.cc:83-85) -- is always byte 15 of the last chunk.
+//  2. Length sort per tile (CSR).  A 256-thread block takes a tile of 512 consecutive
+//     keys, counting-sorts them in LDS by chunk count, and each wave hashes groups of 64
+//     keys of (nearly) the same chunk count.
+//  3. The line ring (ring_hash).  Per-lane loads of 16 B at 64 scattered keys, or even
+//     cooperative loads of 80-byte windows that straddle 128-byte lines, run at 2-3 TB/s
+//     on MI355X (tools/stream_floor2.hip).  Instead every lane's key is streamed as whole
+//     128-byte-aligned lines: each round the wave loads one line per lane cooperatively
+//     (8 lanes x 16 B per line, 8 full lines per load instruction -- 5.7 TB/s in the same
+//     probe) into a 2-line LDS ring per lane, and the lane reads its next 8 chunks from
+//     the ring at its own byte offset.  A line is only ever loaded if it holds a byte of
+//     some key, so no load can leave the buffer's pages and no bounds checks are needed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "k2h_fnv_device.h"
+#include "k2h_kernels.h"
+
+namespace k2h {
+
+namespace {
+
+typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
+typedef uint32_t u32x4_v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4_v gvec4;
+
+__device__ __forceinline__ uint4 ld16(const uint8_t* p) {
+  u32x4_ua v = *reinterpret_cast<const u32x4_ua*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+// 16 bytes at p where bytes below `lo` must not be touched (they are don't-care).
+__device__ __forceinline__ uint4 ld16_lowguard(const uint8_t* p, const uint8_t* lo) {
+  if (p >= lo) return ld16(p);
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (int j = 0; j < 16; ++j)
+    if (p + j >= lo) w[j >> 2] |= (uint32_t)p[j] << (8 * (j & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// Zero the first p (0..15) bytes of a chunk.
+__device__ __forceinline__ uint4 mask_lead(uint4 c, uint32_t p) {
+  uint32_t sh = 8u * p;
+  auto m = [sh](uint32_t base) -> uint32_t {
+    if (sh >= base + 32) return 0u;
+    if (sh <= base) return 0xffffffffu;
+    return 0xffffffffu << (sh - base);
+  };
+  return make_uint4(c.x & m(0), c.y & m(32), c.z & m(64), c.w & m(96));
+}
+
+__device__ __forceinline__ uint64_t pack2(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
+  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)(src_lane << 2), (int)v);
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, uint32_t src_lane) {
+  return ((uint64_t)bperm((uint32_t)(v >> 32), src_lane) << 32) | bperm((uint32_t)v, src_lane);
+}
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+
+// ---------------------------------------------------------------------------
+// Direct per-lane walker (A/B variant kVariantDirect): each lane loads its own chunks.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void hash_key(const uint8_t* s, const uint8_t* e, const uint8_t* lo_bound,
+                                         const uint64_t* spad, uint64_t& r1, uint64_t& r2) {
+  uint64_t len = (uint64_t)(e - s);
+  if (len == 0) {  // lib/k2hashfunc.cc:66-68, 80-82
+    r1 = r2 = 0;
+    return;
+  }
+  uint64_t k = (len + 15) >> 4;
+  uint32_t p = (uint32_t)(16 * k - len);
+  const uint8_t* cp = e - 16 * k;
+  uint64_t st = spad[p];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2, hi2;
+  uint4 c = mask_lead(ld16_lowguard(cp, lo_bound), p);
+  for (uint64_t j = 1; j < k; ++j) {
+    uint4 nx = ld16(cp + 16 * j);
+    fnv_chunk16(lo, hi, c);
+    c = nx;
+  }
+  fnv_chunk16_last(lo, hi, lo2, hi2, c);
+  r1 = pack2(lo, hi);
+  r2 = len == 1 ? r1 : pack2(lo2, hi2);  // length 1: second hash not shortened (lib/k2hashfunc.cc:83)
+}
+
+// ---------------------------------------------------------------------------
+// The line ring.
+// ---------------------------------------------------------------------------
+constexpr int kRingRow = 272;  // 2 x 128-byte slots + 16-byte mirror of slot 0's head
+struct alignas(16) Ring {
+  uint8_t b[64][kRingRow];
+};
+
+// Hash key [s, e) of every valid lane of the wave.  All 64 lanes must call.
+// `safe` is any readable 128-byte-aligned address (used by idle lanes' loads).
+__device__ __forceinline__ void ring_hash(bool valid, const uint8_t* s, const uint8_t* e, uint64_t safe,
+                                          const uint64_t* spad, Ring& ring, uint64_t& r1, uint64_t& r2) {
+  const uint32_t lane = threadIdx.x & 63u;
+  uint64_t len = valid ? (uint64_t)(e - s) : 0;
+  uint32_t k = (uint32_t)((len + 15) >> 4);  // chunks (0: empty key or idle lane)
+  uint32_t p = (uint32_t)(16u * k - len);    // leading pad bytes of chunk 0
+  uint64_t cp = (uint64_t)(uintptr_t)e - 16ull * k;  // chunk 0 (virtual start, may precede s)
+  uint64_t blk0 = cp & ~127ull;
+  uint32_t mis = (uint32_t)(cp & 127u);
+  // lines of this lane's stream that hold key bytes: [first, last] (relative to blk0)
+  uint32_t first = 0, last = 0;
+  if (k) {
+    first = (uint32_t)(((uint64_t)(uintptr_t)s - blk0) >> 7);
+    last = (uint32_t)(((uint64_t)(uintptr_t)e - 1 - blk0) >> 7);
+  } else {
+    blk0 = safe;
+  }
+  const uint32_t rounds = (k + 7) >> 3;
+  const uint32_t R = wave_max(rounds);
+  uint64_t st = spad[p & 15u];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2 = lo, hi2 = hi;
+
+  if (R) {
+    // load instruction j: lane t fetches piece t&7 of line q of lane 8j + t/8
+    const uint32_t piece = lane & 7u;
+    uint64_t jb[8];
+    uint32_t jf[8], jl[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      uint32_t src = 8u * j + (lane >> 3);
+      jb[j] = bperm64(blk0, src) + 16u * piece;
+      jf[j] = bperm(first, src);
+      jl[j] = bperm(last, src);
+    }
+    auto load_line = [&](uint32_t q, uint4 (&v)[8]) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint32_t qq = q < jf[j] ? jf[j] : (q > jl[j] ? jl[j] : q);  // keep to lines holding key bytes
+        u32x4_v x = __builtin_nontemporal_load((gvec4*)(uintptr_t)(jb[j] + 128ull * qq));
+        v[j] = make_uint4(x.x, x.y, x.z, x.w);
+      }
+    };
+    auto store_line = [&](uint32_t q, const uint4 (&v)[8]) {
+      uint32_t off = (q & 1u) * 128u + 16u * piece;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        uint8_t* row = ring.b[8u * j + (lane >> 3)];
+        *reinterpret_cast<uint4*>(row + off) = v[j];
+        if (off == 0) *reinterpret_cast<uint4*>(row + 256) = v[j];  // mirror: reads may wrap
+      }
+    };
+    uint4 va[8], vb[8];
+    load_line(0, va);
+    load_line(1, vb);
+    store_line(0, va);
+    store_line(1, vb);
+    if (R >= 2) load_line(2, va);
+    asm volatile("" ::: "memory");
+    const uint8_t* row = ring.b[lane];
+    for (uint32_t r = 0; r < R; ++r) {
+#pragma unroll
+      for (int m = 0; m < 8; ++m) {
+        uint32_t q = 8u * r + m;
+        if (q < k) {
+          uint4 c = ld16(row + ((mis + 16u * q) & 255u));
+          if (q == 0) c = mask_lead(c, p);
+          if (q + 1 < k) {
+            fnv_chunk16(lo, hi, c);
+          } else {
+            fnv_chunk16_last(lo, hi, lo2, hi2, c);
+          }
+        }
+      }
+      asm volatile("" ::: "memory");  // one wave's LDS ops execute in order; keep the compiler's
+      if (r + 2 <= R) {
+        store_line(r + 2, va);
+        if (r + 3 <= R) load_line(r + 3, va);
+      }
+      asm volatile("" ::: "memory");
+    }
+  }
+  if (k == 0) {  // empty key (lib/k2hashfunc.cc:66-68, 80-82) or idle lane
+    r1 = r2 = 0;
+    return;
+  }
+  r1 = pack2(lo, hi);
+  r2 = len == 1 ? r1 : pack2(lo2, hi2);
+}
+
+// Hash key [s, e) whose bytes are staged in LDS at `lds + (x - tile_base)` for every
+// byte address x of the tile (lds has 16 readable bytes below its start for chunk 0's
+// pad).  Chunk reads are unaligned ds_read_b128.
+__device__ __forceinline__ void lds_hash(bool valid, uint64_t s, uint64_t e, uint64_t tile_base, const uint8_t* lds,
+                                         const uint64_t* spad, uint64_t& r1, uint64_t& r2) {
+  uint64_t len = valid ? e - s : 0;
+  uint32_t k = (uint32_t)((len + 15) >> 4);
+  uint32_t p = (uint32_t)(16u * k - len);
+  const uint8_t* cp = lds + (int64_t)(e - 16ull * k - tile_base);
+  uint64_t st = spad[p & 15u];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2 = lo, hi2 = hi;
+  if (k) {
+    uint4 c = mask_lead(ld16(cp), p);
+    for (uint32_t q = 1; q < k; ++q) {
+      uint4 nx = ld16(cp + 16u * q);
+      fnv_chunk16(lo, hi, c);
+      c = nx;
+    }
+    fnv_chunk16_last(lo, hi, lo2, hi2, c);
+  }
+  if (k == 0) {
+    r1 = r2 = 0;
+    return;
+  }
+  r1 = pack2(lo, hi);
+  r2 = len == 1 ? r1 : pack2(lo2, hi2);
+}
+
+constexpr int kTileKeys = 512;
+constexpr int kBins = 256;
+// LDS image of a whole tile's bytes (staged mode).  Sized so two 256-thread blocks fit a
+// CU (160 KiB) and a tile of 512 keys of BASELINE config 3 (8-256 B, mean 132 B: 67.6 KB
+// per tile, sd 1.7 KB) fits with > 99 % probability; larger tiles take the ring path.
+constexpr int kStageBytes = 73 * 1024;
+union TileLds {
+  Ring ring[4];
+  uint8_t stage[16 + kStageBytes];
+};
+
+// Sort class of a key: its chunk count for up to 127 chunks (2032 B), then 4
+// sub-classes per octave of chunk count.
+__device__ __forceinline__ uint32_t len_bin(uint64_t len) {
+  if (len == 0) return 0;
+  uint64_t k = (len + 15) >> 4;
+  if (k < 128) return (uint32_t)k;
+  uint32_t lg = 63u - (uint32_t)__clzll((long long)k);  // >= 7
+  uint32_t b = 128u + (lg - 7u) * 4u + (uint32_t)((k >> (lg - 2u)) & 3u);
+  return b < (uint32_t)kBins ? b : (uint32_t)kBins - 1u;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// CSR: one 256-thread block per tile of 512 keys.
+// ---------------------------------------------------------------------------
+enum { kModeStaged = 0, kModeDirect = 1, kModeRing = 2 };
+
+template <bool H2, int MODE>
+__global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __restrict__ bytes,
+                                                           const uint64_t* __restrict__ offsets, uint64_t n,
+                                                           SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                           uint64_t* __restrict__ h2) {
+  __shared__ uint64_t s_off[kTileKeys + 1];
+  __shared__ uint16_t s_order[kTileKeys];
+  __shared__ uint32_t s_hist[kBins];
+  __shared__ uint32_t s_wsum[4];
+  __shared__ uint64_t s_spad[16];
+  __shared__ TileLds s_u;
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTileKeys;
+  const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)kTileKeys ? n - t0 : (uint64_t)kTileKeys);
+  const uint8_t* lo_bound = bytes + offsets[0];
+  const uint64_t safe = (uint64_t)(uintptr_t)lo_bound & ~127ull;
+
+  if (tid < 16) s_spad[tid] = spad_tab.v[tid];
+  for (uint32_t k = tid; k <= cnt; k += 256) s_off[k] = offsets[t0 + k];
+  s_hist[tid] = 0;
+  __syncthreads();
+
+  // staged mode: DMA the tile's whole byte span into LDS (lane-linear 1 KiB pieces,
+  // no registers), in flight while the tile is sorted
+  const uint64_t span_lo = ((uint64_t)(uintptr_t)bytes + s_off[0]) & ~15ull;
+  const uint64_t span_hi = (uint64_t)(uintptr_t)bytes + s_off[cnt];
+  const bool staged = MODE == kModeStaged && span_hi - span_lo <= (uint64_t)kStageBytes;
+  if (staged) {
+    const uint32_t npieces = (uint32_t)((span_hi - span_lo + 1023) >> 10);
+    for (uint32_t c = wave; c < npieces; c += 4) {
+      uint64_t src = span_lo + 1024ull * c + 16u * lane;
+      if (src >= span_hi) src = span_lo;  // past the span's last 16-byte piece: re-read a safe one
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(uintptr_t)src,
+                                       (__attribute__((address_space(3))) void*)(s_u.stage + 16 + 1024u * c), 16, 0,
+                                       0);
+    }
+  }
+
+  // 1. histogram of length classes
+  uint32_t bins[kTileKeys / 256];
+#pragma unroll
+  for (int j = 0; j < kTileKeys / 256; ++j) {
+    uint32_t k = tid + 256u * j;
+    if (k < cnt) {
+      bins[j] = len_bin(s_off[k + 1] - s_off[k]);
+      atomicAdd(&s_hist[bins[j]], 1u);
+    }
+  }
+  __syncthreads();
+  // 2. exclusive scan of the 256 class counts (one per thread)
+  uint32_t v = s_hist[tid], incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
+  s_hist[tid] = base + incl - v;  // becomes the scatter cursor
+  __syncthreads();
+  // 3. scatter key indices in class order
+#pragma unroll
+  for (int j = 0; j < kTileKeys / 256; ++j) {
+    uint32_t k = tid + 256u * j;
+    if (k < cnt) s_order[atomicAdd(&s_hist[bins[j]], 1u)] = (uint16_t)k;
+  }
+  __syncthreads();
+  // 4. each wave hashes groups of 64 class-sorted keys; results go straight to global
+  //    (scattered 8-byte stores within the tile's 4 KiB output run merge in L2)
+  if (staged) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces have landed
+    __syncthreads();                                   // ... and every other wave's
+  }
+  const uint32_t ngroups = (cnt + 63u) >> 6;
+  for (uint32_t g = wave; g < ngroups; g += 4) {
+    uint32_t idx = g * 64u + lane;
+    bool valid = idx < cnt;
+    uint32_t k = s_order[valid ? idx : cnt - 1];
+    uint64_t r1 = 0, r2 = 0;
+    if constexpr (MODE == kModeDirect) {
+      if (valid) hash_key(bytes + s_off[k], bytes + s_off[k + 1], lo_bound, s_spad, r1, r2);
+    } else {
+      if (staged)
+        lds_hash(valid, (uint64_t)(uintptr_t)bytes + s_off[k], (uint64_t)(uintptr_t)bytes + s_off[k + 1], span_lo,
+                 s_u.stage + 16, s_spad, r1, r2);
+      else
+        ring_hash(valid, bytes + s_off[k], bytes + s_off[k + 1], safe, s_spad, s_u.ring[wave], r1, r2);
+    }
+    if (valid) {
+      h1[t0 + k] = r1;
+      if constexpr (H2) h2[t0 + k] = r2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-length keys other than the 32-byte fast path (e.g. BASELINE config 5,
+// 4 KiB): one lane per key, the same chunk walker, uniform trip count.
+// ---------------------------------------------------------------------------
+template <bool H2, bool DIRECT>
+__global__ __launch_bounds__(256) void fnv_fixed_long_kernel(const uint8_t* __restrict__ base, uint64_t key_len,
+                                                             uint64_t n, SpadTable spad_tab,
+                                                             uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+  __shared__ uint64_t s_spad[16];
+  __shared__ Ring s_ring[DIRECT ? 1 : 4];
+  if (threadIdx.x < 16) s_spad[threadIdx.x] = spad_tab.v[threadIdx.x];
+  __syncthreads();
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  bool valid = i < n;
+  uint64_t r1, r2;
+  if constexpr (DIRECT) {
+    if (!valid) return;
+    hash_key(base + key_len * i, base + key_len * (i + 1), base, s_spad, r1, r2);
+  } else {
+    if ((uint64_t)blockIdx.x * 256u + (threadIdx.x & ~63u) >= n) return;  // whole wave idle
+    uint64_t ii = valid ? i : n - 1;
+    ring_hash(valid, base + key_len * ii, base + key_len * (ii + 1), (uint64_t)(uintptr_t)base & ~127ull, s_spad,
+              s_ring[threadIdx.x >> 6], r1, r2);
+    if (!valid) return;
+  }
+  __builtin_nontemporal_store(r1, h1 + i);
+  if constexpr (H2) __builtin_nontemporal_store(r2, h2 + i);
+}
+
+// S_p = seed * P^-p mod 2^64, p = 0..15 (P = 1099511628211 is odd, so invertible).
+SpadTable make_spad(uint64_t seed) {
+  const uint64_t P = 1099511628211ULL;
+  uint64_t inv = P;  // Newton: inv = inv * (2 - P*inv); P*P = 1 mod 8, 5 doublings reach 64 bits
+  for (int i = 0; i < 6; ++i) inv *= 2 - P * inv;
+  SpadTable t;
+  uint64_t s = seed;
+  for (int p = 0; p < 16; ++p) {
+    t.v[p] = s;
+    s *= inv;
+  }
+  return t;
+}
+
+hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+                           uint64_t* h2, int mode, hipStream_t stream) {
+  SpadTable t = make_spad(seed);
+  unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
+  const uint8_t* b = (const uint8_t*)bytes;
+#define K2H_CSR_LAUNCH(M)                                                                      \
+  if (h2) fnv_csr_tile_kernel<true, M><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2);       \
+  else fnv_csr_tile_kernel<false, M><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr);
+  switch (mode) {
+    case kModeDirect: K2H_CSR_LAUNCH(kModeDirect) break;
+    case kModeRing: K2H_CSR_LAUNCH(kModeRing) break;
+    default: K2H_CSR_LAUNCH(kModeStaged) break;
+  }
+#undef K2H_CSR_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
+                             uint64_t* h2, bool direct, hipStream_t stream) {
+  SpadTable t = make_spad(seed);
+  unsigned g = (unsigned)((n + 255) / 256);
+  const uint8_t* k = (const uint8_t*)keys;
+  if (direct) {
+    if (h2) fnv_fixed_long_kernel<true, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2);
+    else fnv_fixed_long_kernel<false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr);
+  } else {
+    if (h2) fnv_fixed_long_kernel<true, false><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2);
+    else fnv_fixed_long_kernel<false, false><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace k2h

@@ -15,7 +15,27 @@ enum {
   kVariantCompiler = 1,  // fixed32: compiler-scheduled byte step instead of the hand-scheduled one
   kVariantGeneric = 2,   // fixed32: force the generic any-length kernel
   kVariantSimpleCsr = 3, // csr: one lane per key in input order (no length balancing)
+  kVariantFixed32Flat = 4,     // fixed32: one 256-thread block per 256 keys (no prefetch)
+  kVariantFixed32Persist = 5,  // fixed32: persistent grid, next keys prefetched into registers
+  kVariantFixed32Lds = 6,      // fixed32: persistent + coalesced 1 KiB loads transposed through LDS
+  kVariantFixed32Kpt2 = 7,     // fixed32: flat grid, 2 keys per thread, all loads issued up front
+  kVariantFixed32Kpt4 = 8,     // fixed32: flat grid, 4 keys per thread
+  kVariantFixedTail = 9,       // fixed (non-32): per-lane byte tail loop instead of end-aligned chunks
+  kVariantDirect = 10,         // csr tile / fixed long: per-lane direct loads instead of the line ring
+  kVariantCsrRing = 11,        // csr tile: line ring for every tile (no LDS staging of the tile)
 };
+
+// S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).
+struct SpadTable {
+  uint64_t v[16];
+};
+SpadTable make_spad(uint64_t seed);
+
+// mode: 0 = tile staged in LDS by DMA (ring for oversize tiles), 1 = per-lane direct, 2 = ring only
+hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+                           uint64_t* h2, int mode, hipStream_t stream);
+hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
+                             uint64_t* h2, bool direct, hipStream_t stream);
 
 hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
                         int variant, hipStream_t stream);

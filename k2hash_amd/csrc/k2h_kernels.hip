@@ -54,15 +54,33 @@ __device__ __forceinline__ void fnv_tail(uint32_t& lo, uint32_t& hi, uint32_t& l
 
 __device__ __forceinline__ uint64_t pack(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 
+// Streaming (nontemporal) forms: every key byte is read once and every hash written
+// once, so both bypass cache retention.  Measured on MI355X for the fixed32 access
+// pattern (tools/mem_floor.hip): 104.9 us per 16M keys with nt loads + nt stores vs
+// 114.6 us with default-policy accesses.
+typedef uint32_t u32x4_v __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 ld_nt(const uint4* p) {
+  u32x4_v v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_v*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void st_nt(uint64_t* p, uint64_t v) { __builtin_nontemporal_store(v, p); }
+
 // ---------------------------------------------------------------------------
 // fixed32: key i = keys[32*i .. 32*i+32), keys 16-byte aligned.
 // ---------------------------------------------------------------------------
-template <bool H2, bool ASM>
+template <bool H2, bool ASM, bool NT = false>
 __global__ __launch_bounds__(256) void fnv_fixed32_kernel(const uint4* __restrict__ keys, uint64_t n, uint64_t seed,
                                                           uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
   uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
-  uint4 a = keys[2 * i], b = keys[2 * i + 1];
+  uint4 a, b;
+  if constexpr (NT) {
+    a = ld_nt(keys + 2 * i);
+    b = ld_nt(keys + 2 * i + 1);
+  } else {
+    a = keys[2 * i];
+    b = keys[2 * i + 1];
+  }
   uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2, hi2;
   if constexpr (ASM) {
     if constexpr (H2) {
@@ -83,8 +101,13 @@ __global__ __launch_bounds__(256) void fnv_fixed32_kernel(const uint4* __restric
       fnv_step_c(lo, hi, (w[7] >> (8 * k)) & 0xffu);
     }
   }
-  h1[i] = pack(lo, hi);
-  if constexpr (H2) h2[i] = pack(lo2, hi2);
+  if constexpr (NT) {
+    st_nt(h1 + i, pack(lo, hi));
+    if constexpr (H2) st_nt(h2 + i, pack(lo2, hi2));
+  } else {
+    h1[i] = pack(lo, hi);
+    if constexpr (H2) h2[i] = pack(lo2, hi2);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -122,6 +145,124 @@ __global__ __launch_bounds__(256) void fill_zero_kernel(uint64_t* __restrict__ p
 
 static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
+// ---------------------------------------------------------------------------
+// fixed32, persistent: 8 blocks of 256 threads per CU (8 waves/SIMD), each thread
+// strides over keys and loads its next key while hashing the current one, so a
+// wave's HBM latency hides under its own VALU work as well as other waves'.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void fixed32_hash_store(uint4 a, uint4 b, uint64_t seed, uint64_t i, uint64_t* h1,
+                                                   uint64_t* h2, bool want_h2) {
+  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2, hi2;
+  if (want_h2) {
+    fnv_chunk32_last(lo, hi, lo2, hi2, a, b);
+    h2[i] = pack(lo2, hi2);
+  } else {
+    fnv_chunk32(lo, hi, a, b);
+  }
+  h1[i] = pack(lo, hi);
+}
+
+template <bool H2>
+__global__ __launch_bounds__(256) void fnv_fixed32_persist_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                                  uint64_t seed, uint64_t* __restrict__ h1,
+                                                                  uint64_t* __restrict__ h2) {
+  const uint64_t stride = (uint64_t)gridDim.x * 256u;
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  uint4 a = keys[2 * i], b = keys[2 * i + 1];
+  for (;;) {
+    uint64_t nx = i + stride;
+    bool more = nx < n;
+    uint4 na = a, nb = b;
+    if (more) {
+      na = keys[2 * nx];
+      nb = keys[2 * nx + 1];
+    }
+    fixed32_hash_store(a, b, seed, i, h1, h2, H2);
+    if (!more) break;
+    i = nx;
+    a = na;
+    b = nb;
+  }
+}
+
+// Same, but each wave reads its 64 keys as two fully coalesced 1 KiB loads (lane l:
+// bytes 16l and 1024+16l of the wave's 2 KiB run) and transposes them through a
+// wave-private 2 KiB LDS slot, so every global load instruction touches 8 whole
+// 128-byte lines instead of 16 half lines.
+template <bool H2>
+__global__ __launch_bounds__(256) void fnv_fixed32_lds_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                              uint64_t seed, uint64_t* __restrict__ h1,
+                                                              uint64_t* __restrict__ h2) {
+  __shared__ uint4 slot[4][128];
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const uint64_t waves = (uint64_t)gridDim.x * 4u;
+  const uint64_t ntiles = (n + 63) / 64;
+  uint64_t t = (uint64_t)blockIdx.x * 4u + wave;
+  if (t >= ntiles) return;
+  const uint64_t nchunks = 2 * n;  // 16-byte chunks in the key buffer
+  auto ld = [&](uint64_t tile, uint4& x, uint4& y) {
+    uint64_t c0 = tile * 128 + lane, c1 = c0 + 64;
+    x = c0 < nchunks ? keys[c0] : make_uint4(0, 0, 0, 0);
+    y = c1 < nchunks ? keys[c1] : make_uint4(0, 0, 0, 0);
+  };
+  uint4 x, y;
+  ld(t, x, y);
+  for (;;) {
+    uint64_t nt = t + waves;
+    bool more = nt < ntiles;
+    uint4 nx = x, ny = y;
+    if (more) ld(nt, nx, ny);
+    slot[wave][lane] = x;
+    slot[wave][lane + 64] = y;
+    __builtin_amdgcn_wave_barrier();
+    uint4 a = slot[wave][2 * lane], b = slot[wave][2 * lane + 1];
+    __builtin_amdgcn_wave_barrier();
+    uint64_t i = t * 64 + lane;
+    if (i < n) fixed32_hash_store(a, b, seed, i, h1, h2, H2);
+    if (!more) break;
+    t = nt;
+    x = nx;
+    y = ny;
+  }
+}
+
+// fixed32, flat grid, KPT keys per thread: block b owns keys [b*256*KPT, (b+1)*256*KPT);
+// thread t hashes keys b*256*KPT + j*256 + t.  All 2*KPT loads are issued before the
+// first hash, so each wave keeps KPT*2 KiB in flight while it computes.
+template <bool H2, int KPT>
+__global__ __launch_bounds__(256) void fnv_fixed32_kpt_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                              uint64_t seed, uint64_t* __restrict__ h1,
+                                                              uint64_t* __restrict__ h2) {
+  const uint64_t base = (uint64_t)blockIdx.x * (256u * KPT) + threadIdx.x;
+  uint4 a[KPT], b[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    uint64_t i = base + 256u * j;
+    if (i < n) {
+      a[j] = keys[2 * i];
+      b[j] = keys[2 * i + 1];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    uint64_t i = base + 256u * j;
+    if (i < n) fixed32_hash_store(a[j], b[j], seed, i, h1, h2, H2);
+  }
+}
+
+static unsigned persist_grid(uint64_t units_of_256) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  uint64_t g = (uint64_t)cus * 8;  // 8 x 256-thread blocks = 32 waves per CU
+  return (unsigned)(units_of_256 < g ? units_of_256 : g);
+}
+
 hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
                         int variant, hipStream_t stream) {
   if (n == 0) return hipSuccess;
@@ -133,16 +274,48 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
   bool aligned16 = ((uintptr_t)keys & 15u) == 0;
   if (key_len == 32 && aligned16 && variant != kVariantGeneric) {
     const uint4* k = (const uint4*)keys;
-    bool use_asm = variant != kVariantCompiler;
-    if (h2) {
-      if (use_asm) fnv_fixed32_kernel<true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
-      else fnv_fixed32_kernel<true, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
-    } else {
-      if (use_asm) fnv_fixed32_kernel<false, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
-      else fnv_fixed32_kernel<false, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
+    switch (variant) {
+      case kVariantCompiler:
+        if (h2) fnv_fixed32_kernel<true, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_kernel<false, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      case kVariantAuto:
+        if (h2) fnv_fixed32_kernel<true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_kernel<false, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      case kVariantFixed32Flat:
+        if (h2) fnv_fixed32_kernel<true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_kernel<false, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      case kVariantFixed32Kpt2: {
+        unsigned g = (unsigned)((n + 511) / 512);
+        if (h2) fnv_fixed32_kpt_kernel<true, 2><<<g, 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_kpt_kernel<false, 2><<<g, 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
+      case kVariantFixed32Kpt4: {
+        unsigned g = (unsigned)((n + 1023) / 1024);
+        if (h2) fnv_fixed32_kpt_kernel<true, 4><<<g, 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_kpt_kernel<false, 4><<<g, 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
+      case kVariantFixed32Lds: {
+        unsigned g = persist_grid((n + 255) / 256);
+        if (h2) fnv_fixed32_lds_kernel<true><<<g, 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_lds_kernel<false><<<g, 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
+      default: {  // kVariantFixed32Persist
+        unsigned g = persist_grid((n + 255) / 256);
+        if (h2) fnv_fixed32_persist_kernel<true><<<g, 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_persist_kernel<false><<<g, 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
     }
     return hipGetLastError();
   }
+  if (variant != kVariantFixedTail)
+    return launch_fixed_long(keys, key_len, n, seed, h1, h2, variant == kVariantDirect, stream);
   if (h2) fnv_fixed_kernel<true><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)keys, key_len, n, seed, h1, h2);
   else fnv_fixed_kernel<false><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)keys, key_len, n, seed, h1, nullptr);
   return hipGetLastError();
@@ -198,8 +371,10 @@ hipError_t launch_csr_simple(const void* bytes, const uint64_t* offsets, uint64_
 
 hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                       uint64_t* h2, int variant, hipStream_t stream) {
-  (void)variant;
-  return launch_csr_simple(bytes, offsets, n, seed, h1, h2, stream);
+  if (n == 0) return hipSuccess;
+  if (variant == kVariantSimpleCsr || !bytes) return launch_csr_simple(bytes, offsets, n, seed, h1, h2, stream);
+  return launch_csr_tile(bytes, offsets, n, seed, h1, h2,
+                         variant == kVariantDirect ? 1 : (variant == kVariantCsrRing ? 2 : 0), stream);
 }
 
 }  // namespace k2h
