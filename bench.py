@@ -47,6 +47,7 @@ def parse():
     p.add_argument("--gather", action="store_true", help="also time the RCCL gather of hashes (N>1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--variant", type=int, default=0, help="kernel variant (A/B knob, 0 = auto)")
+    p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
     return p.parse_args()
 
 
@@ -97,10 +98,14 @@ def main():
         if world == 1 and args.gpus > 1:
             print("for --gpus N > 1 launch with torch.distributed.run (one process per GPU)", file=sys.stderr)
             sys.exit(2)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))  # one process per GPU; wraps only in rehearsals
     torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
     batch.set_variant(args.variant)
 
     kind, n, shape, desc = CONFIGS[args.config]

@@ -69,6 +69,14 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
 __device__ __forceinline__ uint64_t bperm64(uint64_t v, uint32_t src_lane) {
   return ((uint64_t)bperm((uint32_t)(v >> 32), src_lane) << 32) | bperm((uint32_t)v, src_lane);
 }
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64);
+    v = o < v ? o : v;
+  }
+  return v;
+}
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
@@ -206,23 +214,42 @@ __device__ __forceinline__ void ring_hash(bool valid, const uint8_t* s, const ui
 // Hash key [s, e) whose bytes are staged in LDS at `lds + (x - tile_base)` for every
 // byte address x of the tile (lds has 16 readable bytes below its start for chunk 0's
 // pad).  Chunk reads are unaligned ds_read_b128.
+template <int WALK>  // 1: one chunk per statement (default), 0: uniform asm run + divergent tail, 2: pairs
 __device__ __forceinline__ void lds_hash(bool valid, uint64_t s, uint64_t e, uint64_t tile_base, const uint8_t* lds,
                                          const uint64_t* spad, uint64_t& r1, uint64_t& r2) {
   uint64_t len = valid ? e - s : 0;
   uint32_t k = (uint32_t)((len + 15) >> 4);
   uint32_t p = (uint32_t)(16u * k - len);
-  const uint8_t* cp = lds + (int64_t)(e - 16ull * k - tile_base);
+  // idle / empty-key lanes walk from the stage start (harmless reads, result discarded)
+  const uint8_t* cp = k ? lds + (int64_t)(e - 16ull * k - tile_base) : lds;
   uint64_t st = spad[p & 15u];
   uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2 = lo, hi2 = hi;
-  if (k) {
-    uint4 c = mask_lead(ld16(cp), p);
-    for (uint32_t q = 1; q < k; ++q) {
-      uint4 nx = ld16(cp + 16u * q);
-      fnv_chunk16(lo, hi, c);
-      c = nx;
+  // chunk j of the key is at cp + 16 j; body chunks 0..k-2, then the last chunk k-1
+  // takes the snapshot for the second hash
+  uint4 c0 = mask_lead(ld16(cp), p);
+  uint32_t j = 0;
+  if constexpr (WALK == 0) {
+    // body chunks every lane has: a wave-uniform asm run
+    uint32_t kmin = wave_min(k ? k : 0xffffffffu);
+    if (kmin != 0xffffffffu && kmin >= 2) {
+      uint32_t run = __builtin_amdgcn_readfirstlane(kmin - 1);
+      fnv_lds_run(lo, hi, c0, (uint32_t)(uintptr_t)(cp + 16), run);
+      j = run;
     }
-    fnv_chunk16_last(lo, hi, lo2, hi2, c);
   }
+  if constexpr (WALK == 2) {
+    for (; j + 2 < k; j += 2) {
+      uint4 c1 = ld16(cp + 16u * (j + 1)), c2 = ld16(cp + 16u * (j + 2));
+      fnv_chunk32(lo, hi, c0, c1);
+      c0 = c2;
+    }
+  }
+  for (; j + 1 < k; ++j) {
+    uint4 c1 = ld16(cp + 16u * (j + 1));
+    fnv_chunk16(lo, hi, c0);
+    c0 = c1;
+  }
+  fnv_chunk16_last(lo, hi, lo2, hi2, c0);
   if (k == 0) {
     r1 = r2 = 0;
     return;
@@ -258,7 +285,7 @@ __device__ __forceinline__ uint32_t len_bin(uint64_t len) {
 // ---------------------------------------------------------------------------
 // CSR: one 256-thread block per tile of 512 keys.
 // ---------------------------------------------------------------------------
-enum { kModeStaged = 0, kModeDirect = 1, kModeRing = 2 };
+enum { kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4 };
 
 template <bool H2, int MODE>
 __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __restrict__ bytes,
@@ -287,7 +314,8 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
   // no registers), in flight while the tile is sorted
   const uint64_t span_lo = ((uint64_t)(uintptr_t)bytes + s_off[0]) & ~15ull;
   const uint64_t span_hi = (uint64_t)(uintptr_t)bytes + s_off[cnt];
-  const bool staged = MODE == kModeStaged && span_hi - span_lo <= (uint64_t)kStageBytes;
+  const bool staged = (MODE == kModeStaged || MODE == kModeStagedPairs || MODE == kModeStagedSingle) &&
+                      span_hi - span_lo <= (uint64_t)kStageBytes;
   if (staged) {
     const uint32_t npieces = (uint32_t)((span_hi - span_lo + 1023) >> 10);
     for (uint32_t c = wave; c < npieces; c += 4) {
@@ -336,8 +364,12 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces have landed
     __syncthreads();                                   // ... and every other wave's
   }
+  // Groups are in length order, so wave w takes groups w, 7-w, 8+w, 15-w, ... (snake):
+  // every wave gets the same total work and the block's waves finish together.
   const uint32_t ngroups = (cnt + 63u) >> 6;
-  for (uint32_t g = wave; g < ngroups; g += 4) {
+  for (uint32_t it = 0; it * 4 < ngroups; ++it) {
+    uint32_t g = it * 4 + ((it & 1) ? 3 - wave : wave);
+    if (g >= ngroups) continue;
     uint32_t idx = g * 64u + lane;
     bool valid = idx < cnt;
     uint32_t k = s_order[valid ? idx : cnt - 1];
@@ -346,7 +378,7 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
       if (valid) hash_key(bytes + s_off[k], bytes + s_off[k + 1], lo_bound, s_spad, r1, r2);
     } else {
       if (staged)
-        lds_hash(valid, (uint64_t)(uintptr_t)bytes + s_off[k], (uint64_t)(uintptr_t)bytes + s_off[k + 1], span_lo,
+        lds_hash<MODE == kModeStagedSingle ? 0 : MODE == kModeStagedPairs ? 2 : 1>(valid, (uint64_t)(uintptr_t)bytes + s_off[k], (uint64_t)(uintptr_t)bytes + s_off[k + 1], span_lo,
                  s_u.stage + 16, s_spad, r1, r2);
       else
         ring_hash(valid, bytes + s_off[k], bytes + s_off[k + 1], safe, s_spad, s_u.ring[wave], r1, r2);
@@ -412,6 +444,8 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
   switch (mode) {
     case kModeDirect: K2H_CSR_LAUNCH(kModeDirect) break;
     case kModeRing: K2H_CSR_LAUNCH(kModeRing) break;
+    case kModeStagedPairs: K2H_CSR_LAUNCH(kModeStagedPairs) break;
+    case kModeStagedSingle: K2H_CSR_LAUNCH(kModeStagedSingle) break;
     default: K2H_CSR_LAUNCH(kModeStaged) break;
   }
 #undef K2H_CSR_LAUNCH

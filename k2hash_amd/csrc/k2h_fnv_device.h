@@ -135,3 +135,129 @@ __device__ __forceinline__ void fnv_chunk32_last(uint32_t& lo, uint32_t& hi, uin
 }
 
 }  // namespace k2h
+
+// ---------------------------------------------------------------------------
+// Whole-key statement for 32-byte keys (fixed32 fast path): the two 16-byte loads, all
+// 32 byte steps and the store in ONE asm statement over explicit registers, so that
+//  - each pair of words gets its sign smear from one 64-bit shift + two v_perm_b32
+//    (3 slow-issue ops per 8 bytes instead of 4), which needs the words in adjacent
+//    registers -- something operand constraints cannot express;
+//  - no moves in or out of the register window.
+// Register window: v[40:47] key words, v48/v49 state, v50 = 0, v51 t, v52 x_lo,
+// v53 m, v54/v58 smears, v[56:57] shifted pair, v[60:61] second-hash snapshot.
+// ---------------------------------------------------------------------------
+namespace k2h {
+
+#define K2H_X_STEP(W, U, K)                                                                            \
+  "v_xor_b32_sdwa v52, sext(" W "), v48 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #K         \
+  " src1_sel:DWORD\n\t"                                                                                \
+  "v_xor_b32_sdwa v49, sext(" U "), v49 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #K          \
+  " src1_sel:DWORD\n\t"                                                                                \
+  "v_mul_lo_u32 v53, v49, %[p]\n\t"                                                                    \
+  "v_lshl_add_u32 v51, v52, 8, v53\n\t"                                                                \
+  "v_mad_u64_u32 v[48:49], vcc, v52, %[p], v[50:51]\n\t"
+#define K2H_X_WORD(W, U) K2H_X_STEP(W, U, 0) K2H_X_STEP(W, U, 1) K2H_X_STEP(W, U, 2) K2H_X_STEP(W, U, 3)
+#define K2H_X_SMEAR2(LO, HI, PAIR)                 \
+  "v_lshlrev_b64 v[56:57], 8, " PAIR "\n\t"        \
+  "v_perm_b32 v54, v56, " LO ", %[sel]\n\t"        \
+  "v_perm_b32 v58, v57, " HI ", %[sel]\n\t"
+#define K2H_X_PAIR(LO, HI, PAIR) K2H_X_SMEAR2(LO, HI, PAIR) K2H_X_WORD(LO, "v54") K2H_X_WORD(HI, "v58")
+#define K2H_X_PAIR_LAST(LO, HI, PAIR)                                                                      \
+  K2H_X_SMEAR2(LO, HI, PAIR) K2H_X_WORD(LO, "v54") K2H_X_STEP(HI, "v58", 0) K2H_X_STEP(HI, "v58", 1)        \
+      K2H_X_STEP(HI, "v58", 2) "v_mov_b32 v60, v48\n\tv_mov_b32 v61, v49\n\t" K2H_X_STEP(HI, "v58", 3)
+#define K2H_X_HEAD                                                     \
+  "global_load_dwordx4 v[40:43], %[src], off nt\n\t"                   \
+  "global_load_dwordx4 v[44:47], %[src], off offset:16 nt\n\t"         \
+  "v_mov_b32 v48, %[slo]\n\t"                                          \
+  "v_mov_b32 v49, %[shi]\n\t"                                          \
+  "v_mov_b32 v50, 0\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"
+#define K2H_X_BODY                                                                                      \
+  K2H_X_PAIR("v40", "v41", "v[40:41]") K2H_X_PAIR("v42", "v43", "v[42:43]") K2H_X_PAIR("v44", "v45", "v[44:45]")
+#define K2H_X_CLOBBERS                                                                                   \
+  "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", \
+      "v55", "v56", "v57", "v58", "v59", "v60", "v61", "vcc", "memory"
+
+// h1 only
+__device__ __forceinline__ void fnv_key32_x(const void* src, uint64_t* dst1, uint64_t seed) {
+  asm volatile(K2H_X_HEAD K2H_X_BODY K2H_X_PAIR("v46", "v47", "v[46:47]")
+               "global_store_dwordx2 %[d1], v[48:49], off nt\n\t"
+               "s_nop 1\n\t"
+               :
+               : [src] "v"(src), [d1] "v"(dst1), [slo] "s"((uint32_t)seed), [shi] "s"((uint32_t)(seed >> 32)),
+                 [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+               : K2H_X_CLOBBERS);
+}
+
+// h1 + h2
+__device__ __forceinline__ void fnv_key32_x2(const void* src, uint64_t* dst1, uint64_t* dst2, uint64_t seed) {
+  asm volatile(K2H_X_HEAD K2H_X_BODY K2H_X_PAIR_LAST("v46", "v47", "v[46:47]")
+               "global_store_dwordx2 %[d1], v[48:49], off nt\n\t"
+               "global_store_dwordx2 %[d2], v[60:61], off nt\n\t"
+               "s_nop 1\n\t"
+               :
+               : [src] "v"(src), [d1] "v"(dst1), [d2] "v"(dst2), [slo] "s"((uint32_t)seed),
+                 [shi] "s"((uint32_t)(seed >> 32)), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+               : K2H_X_CLOBBERS);
+}
+
+}  // namespace k2h
+
+// ---------------------------------------------------------------------------
+// Wave-uniform run over chunks staged in LDS: hashes `cnt` (>= 1, the same in every
+// lane) consecutive chunks -- the one already in `c`, then cnt-1 read from LDS at
+// `lds` (byte address of the chunk after `c`) -- as ONE asm statement: the state stays
+// in v48/v49, chunks alternate between v[40:43] and v[44:47] (no copies), the next
+// chunk's ds_read_b128 is in flight under the current chunk's steps, and each pair of
+// words takes its sign smear from one 64-bit shift + two v_perm_b32.  On return `c`
+// holds the chunk that follows the run (read from LDS, not hashed).
+// ---------------------------------------------------------------------------
+namespace k2h {
+
+#define K2H_X_CHUNK_A K2H_X_PAIR("v40", "v41", "v[40:41]") K2H_X_PAIR("v42", "v43", "v[42:43]")
+#define K2H_X_CHUNK_B K2H_X_PAIR("v44", "v45", "v[44:45]") K2H_X_PAIR("v46", "v47", "v[46:47]")
+
+__device__ __forceinline__ void fnv_lds_run(uint32_t& lo, uint32_t& hi, uint4& c, uint32_t lds, uint32_t cnt) {
+  asm volatile(
+      "v_mov_b32 v48, %[lo]\n\t"
+      "v_mov_b32 v49, %[hi]\n\t"
+      "v_mov_b32 v50, 0\n\t"
+      "v_mov_b32 v40, %[c0]\n\t"
+      "v_mov_b32 v41, %[c1]\n\t"
+      "v_mov_b32 v42, %[c2]\n\t"
+      "v_mov_b32 v43, %[c3]\n\t"
+      "v_mov_b32 v62, %[lds]\n\t"
+      "s_waitcnt lgkmcnt(0)\n"
+      "k2h_run_loop_%=:\n\t"
+      "ds_read_b128 v[44:47], v62\n\t" K2H_X_CHUNK_A
+      "s_sub_u32 %[cnt], %[cnt], 1\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_cmp_eq_u32 %[cnt], 0\n\t"
+      "s_cbranch_scc1 k2h_run_exit_b_%=\n\t"
+      "ds_read_b128 v[40:43], v62 offset:16\n\t" K2H_X_CHUNK_B
+      "v_add_u32_e32 v62, 32, v62\n\t"
+      "s_sub_u32 %[cnt], %[cnt], 1\n\t"
+      "s_waitcnt lgkmcnt(0)\n\t"
+      "s_cmp_eq_u32 %[cnt], 0\n\t"
+      "s_cbranch_scc0 k2h_run_loop_%=\n\t"
+      "v_mov_b32 %[c0], v40\n\t"
+      "v_mov_b32 %[c1], v41\n\t"
+      "v_mov_b32 %[c2], v42\n\t"
+      "v_mov_b32 %[c3], v43\n\t"
+      "s_branch k2h_run_end_%=\n"
+      "k2h_run_exit_b_%=:\n\t"
+      "v_mov_b32 %[c0], v44\n\t"
+      "v_mov_b32 %[c1], v45\n\t"
+      "v_mov_b32 %[c2], v46\n\t"
+      "v_mov_b32 %[c3], v47\n"
+      "k2h_run_end_%=:\n\t"
+      "v_mov_b32 %[lo], v48\n\t"
+      "v_mov_b32 %[hi], v49\n\t"
+      : [lo] "+v"(lo), [hi] "+v"(hi), [c0] "+v"(c.x), [c1] "+v"(c.y), [c2] "+v"(c.z), [c3] "+v"(c.w),
+        [cnt] "+s"(cnt)
+      : [lds] "v"(lds), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+      : "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54",
+        "v55", "v56", "v57", "v58", "v62", "vcc", "scc", "memory");
+}
+
+}  // namespace k2h

@@ -23,6 +23,10 @@ enum {
   kVariantFixedTail = 9,       // fixed (non-32): per-lane byte tail loop instead of end-aligned chunks
   kVariantDirect = 10,         // csr tile / fixed long: per-lane direct loads instead of the line ring
   kVariantCsrRing = 11,        // csr tile: line ring for every tile (no LDS staging of the tile)
+  kVariantFixed32Asm = 12,     // fixed32: whole key (loads, 32 steps, store) in one asm statement
+  kVariantCsrSingle = 13,      // csr staged: wave-uniform asm run over common chunks (lower VALU count,
+                               // more dependency stalls at 2 waves/SIMD: slower, kept for A/B)
+  kVariantCsrPairs = 14,       // csr staged: two chunks per asm statement (no uniform asm run)
 };
 
 // S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).

@@ -110,6 +110,17 @@ __global__ __launch_bounds__(256) void fnv_fixed32_kernel(const uint4* __restric
   }
 }
 
+// fixed32, whole key in one asm statement (fnv_key32_x): explicit registers, 64-bit
+// shift sign smear, nt load/store inside the statement.
+template <bool H2>
+__global__ __launch_bounds__(256) void fnv_fixed32_x_kernel(const uint4* __restrict__ keys, uint64_t n, uint64_t seed,
+                                                            uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  if constexpr (H2) fnv_key32_x2(keys + 2 * i, h1 + i, h2 + i, seed);
+  else fnv_key32_x(keys + 2 * i, h1 + i, seed);
+}
+
 // ---------------------------------------------------------------------------
 // fixed: key i = base[L*i .. L*i+L), any L >= 1, any alignment.  The loop trip
 // count is wave-uniform (L is a kernel argument), so no lane diverges.
@@ -283,6 +294,10 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
         if (h2) fnv_fixed32_kernel<true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_kernel<false, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
+      case kVariantFixed32Asm:
+        if (h2) fnv_fixed32_x_kernel<true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_x_kernel<false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
       case kVariantFixed32Flat:
         if (h2) fnv_fixed32_kernel<true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_kernel<false, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
@@ -374,7 +389,7 @@ hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, ui
   if (n == 0) return hipSuccess;
   if (variant == kVariantSimpleCsr || !bytes) return launch_csr_simple(bytes, offsets, n, seed, h1, h2, stream);
   return launch_csr_tile(bytes, offsets, n, seed, h1, h2,
-                         variant == kVariantDirect ? 1 : (variant == kVariantCsrRing ? 2 : 0), stream);
+                         variant == kVariantDirect ? 1 : variant == kVariantCsrRing ? 2 : variant == kVariantCsrPairs ? 3 : variant == kVariantCsrSingle ? 4 : 0, stream);
 }
 
 }  // namespace k2h

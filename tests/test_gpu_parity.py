@@ -16,7 +16,7 @@ from k2hash_amd import batch
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2, 3]
+VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12]
 
 
 def dev_u8(torch, arr, device, pad_front=0):
