@@ -52,11 +52,13 @@ __device__ __forceinline__ uint4 ld16_lowguard(const uint8_t* p, const uint8_t* 
 
 // Zero the first p (0..15) bytes of a chunk.
 __device__ __forceinline__ uint4 mask_lead(uint4 c, uint32_t p) {
-  uint32_t sh = 8u * p;
-  auto m = [sh](uint32_t base) -> uint32_t {
-    if (sh >= base + 32) return 0u;
-    if (sh <= base) return 0xffffffffu;
-    return 0xffffffffu << (sh - base);
+  // word mask = low half of (~0 << clamp(8p - base, 0, 32)): sub, med3, 64-bit shift
+  // (a 32-bit shift cannot produce the all-zero mask), no compares or selects
+  int32_t sh = (int32_t)(8u * p);
+  auto m = [sh](int32_t base) -> uint32_t {
+    int32_t t = sh - base;
+    t = t < 0 ? 0 : (t > 32 ? 32 : t);
+    return (uint32_t)(~0ull << t);
   };
   return make_uint4(c.x & m(0), c.y & m(32), c.z & m(64), c.w & m(96));
 }
@@ -244,11 +246,23 @@ __device__ __forceinline__ void lds_hash(bool valid, uint64_t s, uint64_t e, uin
       c0 = c2;
     }
   }
-  for (; j + 1 < k; ++j) {
-    uint4 c1 = ld16(cp + 16u * (j + 1));
-    fnv_chunk16(lo, hi, c0);
-    c0 = c1;
+  // two chunks per trip, alternating register banks (no copies between the read of
+  // the next chunk and its hash); the read for the chunk after is in flight meanwhile
+  // (a lane may stop after either half, so a wave whose lanes differ by one chunk still
+  // costs max(k) - 1 body chunks; the last chunk is then in c1 or c0)
+  uint4 c1 = c0;
+  bool odd = false;
+  for (; j + 1 < k; j += 2) {
+    c1 = ld16(cp + 16u * (j + 1));
+    fnv_chunk16<0>(lo, hi, c0);
+    if (j + 2 >= k) {
+      odd = true;
+      break;
+    }
+    c0 = ld16(cp + 16u * (j + 2));
+    fnv_chunk16<1>(lo, hi, c1);
   }
+  if (odd) c0 = c1;
   fnv_chunk16_last(lo, hi, lo2, hi2, c0);
   if (k == 0) {
     r1 = r2 = 0;
@@ -285,7 +299,14 @@ __device__ __forceinline__ uint32_t len_bin(uint64_t len) {
 // ---------------------------------------------------------------------------
 // CSR: one 256-thread block per tile of 512 keys.
 // ---------------------------------------------------------------------------
-enum { kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4 };
+enum { kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5 };
+
+// Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
+// wall clock per block at the phase boundaries, and each wave's finish time.
+#define K2H_PROF_STAMP(SLOT)                                                               \
+  if constexpr (MODE == kModeStagedProf) {                                                 \
+    if (tid == 0) prof[(uint64_t)blockIdx.x * 16u + (SLOT)] = __builtin_amdgcn_s_memrealtime(); \
+  }
 
 template <bool H2, int MODE>
 __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __restrict__ bytes,
@@ -301,6 +322,9 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
   const uint64_t t0 = (uint64_t)blockIdx.x * kTileKeys;
+  uint64_t* const prof = h2;  // profiling mode only: h2 is the stamp buffer (16 per block)
+  (void)prof;
+  K2H_PROF_STAMP(0)
   const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)kTileKeys ? n - t0 : (uint64_t)kTileKeys);
   const uint8_t* lo_bound = bytes + offsets[0];
   const uint64_t safe = (uint64_t)(uintptr_t)lo_bound & ~127ull;
@@ -309,15 +333,18 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
   for (uint32_t k = tid; k <= cnt; k += 256) s_off[k] = offsets[t0 + k];
   s_hist[tid] = 0;
   __syncthreads();
+  K2H_PROF_STAMP(1)
 
   // staged mode: DMA the tile's whole byte span into LDS (lane-linear 1 KiB pieces,
   // no registers), in flight while the tile is sorted
   const uint64_t span_lo = ((uint64_t)(uintptr_t)bytes + s_off[0]) & ~15ull;
   const uint64_t span_hi = (uint64_t)(uintptr_t)bytes + s_off[cnt];
-  const bool staged = (MODE == kModeStaged || MODE == kModeStagedPairs || MODE == kModeStagedSingle) &&
+  const bool staged = (MODE == kModeStaged || MODE == kModeStagedPairs || MODE == kModeStagedSingle ||
+                       MODE == kModeStagedProf) &&
                       span_hi - span_lo <= (uint64_t)kStageBytes;
   if (staged) {
-    const uint32_t npieces = (uint32_t)((span_hi - span_lo + 1023) >> 10);
+    // a tile of empty keys has no bytes to stage (and `bytes` need not point anywhere)
+    const uint32_t npieces = s_off[cnt] > s_off[0] ? (uint32_t)((span_hi - span_lo + 1023) >> 10) : 0u;
     for (uint32_t c = wave; c < npieces; c += 4) {
       uint64_t src = span_lo + 1024ull * c + 16u * lane;
       if (src >= span_hi) src = span_lo;  // past the span's last 16-byte piece: re-read a safe one
@@ -327,6 +354,7 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
     }
   }
 
+  K2H_PROF_STAMP(10)
   // 1. histogram of length classes
   uint32_t bins[kTileKeys / 256];
 #pragma unroll
@@ -338,6 +366,7 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
     }
   }
   __syncthreads();
+  K2H_PROF_STAMP(11)
   // 2. exclusive scan of the 256 class counts (one per thread)
   uint32_t v = s_hist[tid], incl = v;
 #pragma unroll
@@ -351,6 +380,7 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
   for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
   s_hist[tid] = base + incl - v;  // becomes the scatter cursor
   __syncthreads();
+  K2H_PROF_STAMP(12)
   // 3. scatter key indices in class order
 #pragma unroll
   for (int j = 0; j < kTileKeys / 256; ++j) {
@@ -360,10 +390,12 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
   __syncthreads();
   // 4. each wave hashes groups of 64 class-sorted keys; results go straight to global
   //    (scattered 8-byte stores within the tile's 4 KiB output run merge in L2)
+  K2H_PROF_STAMP(2)
   if (staged) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces have landed
     __syncthreads();                                   // ... and every other wave's
   }
+  K2H_PROF_STAMP(3)
   // Groups are in length order, so wave w takes groups w, 7-w, 8+w, 15-w, ... (snake):
   // every wave gets the same total work and the block's waves finish together.
   const uint32_t ngroups = (cnt + 63u) >> 6;
@@ -386,6 +418,19 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
     if (valid) {
       h1[t0 + k] = r1;
       if constexpr (H2) h2[t0 + k] = r2;
+    }
+  }
+  if constexpr (MODE == kModeStagedProf) {
+    if (lane == 0) {
+      uint32_t hw;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      prof[(uint64_t)blockIdx.x * 16u + 4u + wave] = __builtin_amdgcn_s_memrealtime();
+      if (wave == 0) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        prof[(uint64_t)blockIdx.x * 16u + 8u] = ((uint64_t)xcc << 32) | hw;
+        prof[(uint64_t)blockIdx.x * 16u + 9u] = staged;
+      }
     }
   }
 }
@@ -446,6 +491,10 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
     case kModeRing: K2H_CSR_LAUNCH(kModeRing) break;
     case kModeStagedPairs: K2H_CSR_LAUNCH(kModeStagedPairs) break;
     case kModeStagedSingle: K2H_CSR_LAUNCH(kModeStagedSingle) break;
+    case kModeStagedProf:  // h2 = stamp buffer of 16 x ceil(n/512) words, required
+      if (!h2) return hipErrorInvalidValue;
+      fnv_csr_tile_kernel<false, kModeStagedProf><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2);
+      break;
     default: K2H_CSR_LAUNCH(kModeStaged) break;
   }
 #undef K2H_CSR_LAUNCH

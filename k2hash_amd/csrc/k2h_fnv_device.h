@@ -95,59 +95,6 @@ __device__ __forceinline__ void fnv_word_c(uint32_t& lo, uint32_t& hi, uint32_t 
 #define K2H_ASM_SNAP "v_mov_b32 %[lo2], v48\n\tv_mov_b32 %[hi2], v49\n\t"
 #define K2H_ASM_CLOBBERS "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "vcc"
 
-// 16 bytes (one uint4 chunk) into the state.
-__device__ __forceinline__ void fnv_chunk16(uint32_t& lo, uint32_t& hi, uint4 c) {
-  asm(K2H_ASM_BEGIN K2H_ASM_WORD(w0) K2H_ASM_WORD(w1) K2H_ASM_WORD(w2) K2H_ASM_WORD(w3) K2H_ASM_END
-      : [lo] "+v"(lo), [hi] "+v"(hi)
-      : [w0] "v"(c.x), [w1] "v"(c.y), [w2] "v"(c.z), [w3] "v"(c.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
-      : K2H_ASM_CLOBBERS);
-}
-
-// 32 bytes (two chunks), one statement.
-__device__ __forceinline__ void fnv_chunk32(uint32_t& lo, uint32_t& hi, uint4 a, uint4 b) {
-  asm(K2H_ASM_BEGIN K2H_ASM_WORD(w0) K2H_ASM_WORD(w1) K2H_ASM_WORD(w2) K2H_ASM_WORD(w3)
-          K2H_ASM_WORD(w4) K2H_ASM_WORD(w5) K2H_ASM_WORD(w6) K2H_ASM_WORD(w7) K2H_ASM_END
-      : [lo] "+v"(lo), [hi] "+v"(hi)
-      : [w0] "v"(a.x), [w1] "v"(a.y), [w2] "v"(a.z), [w3] "v"(a.w), [w4] "v"(b.x), [w5] "v"(b.y),
-        [w6] "v"(b.z), [w7] "v"(b.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
-      : K2H_ASM_CLOBBERS);
-}
-
-// Last 16-byte chunk of a key: also returns the state before the final byte
-// (the reference's second hash, lib/k2hashfunc.cc:83-85).
-__device__ __forceinline__ void fnv_chunk16_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4 c) {
-  asm(K2H_ASM_BEGIN K2H_ASM_WORD(w0) K2H_ASM_WORD(w1) K2H_ASM_WORD(w2) K2H_ASM_SMEAR(w3) K2H_ASM_STEP(w3, 0)
-          K2H_ASM_STEP(w3, 1) K2H_ASM_STEP(w3, 2) K2H_ASM_SNAP K2H_ASM_STEP(w3, 3) K2H_ASM_END
-      : [lo] "+v"(lo), [hi] "+v"(hi), [lo2] "=&v"(lo2), [hi2] "=&v"(hi2)
-      : [w0] "v"(c.x), [w1] "v"(c.y), [w2] "v"(c.z), [w3] "v"(c.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
-      : K2H_ASM_CLOBBERS);
-}
-
-__device__ __forceinline__ void fnv_chunk32_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4 a,
-                                                 uint4 b) {
-  asm(K2H_ASM_BEGIN K2H_ASM_WORD(w0) K2H_ASM_WORD(w1) K2H_ASM_WORD(w2) K2H_ASM_WORD(w3) K2H_ASM_WORD(w4)
-          K2H_ASM_WORD(w5) K2H_ASM_WORD(w6) K2H_ASM_SMEAR(w7) K2H_ASM_STEP(w7, 0) K2H_ASM_STEP(w7, 1)
-              K2H_ASM_STEP(w7, 2) K2H_ASM_SNAP K2H_ASM_STEP(w7, 3) K2H_ASM_END
-      : [lo] "+v"(lo), [hi] "+v"(hi), [lo2] "=&v"(lo2), [hi2] "=&v"(hi2)
-      : [w0] "v"(a.x), [w1] "v"(a.y), [w2] "v"(a.z), [w3] "v"(a.w), [w4] "v"(b.x), [w5] "v"(b.y),
-        [w6] "v"(b.z), [w7] "v"(b.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
-      : K2H_ASM_CLOBBERS);
-}
-
-}  // namespace k2h
-
-// ---------------------------------------------------------------------------
-// Whole-key statement for 32-byte keys (fixed32 fast path): the two 16-byte loads, all
-// 32 byte steps and the store in ONE asm statement over explicit registers, so that
-//  - each pair of words gets its sign smear from one 64-bit shift + two v_perm_b32
-//    (3 slow-issue ops per 8 bytes instead of 4), which needs the words in adjacent
-//    registers -- something operand constraints cannot express;
-//  - no moves in or out of the register window.
-// Register window: v[40:47] key words, v48/v49 state, v50 = 0, v51 t, v52 x_lo,
-// v53 m, v54/v58 smears, v[56:57] shifted pair, v[60:61] second-hash snapshot.
-// ---------------------------------------------------------------------------
-namespace k2h {
-
 #define K2H_X_STEP(W, U, K)                                                                            \
   "v_xor_b32_sdwa v52, sext(" W "), v48 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #K         \
   " src1_sel:DWORD\n\t"                                                                                \
@@ -165,6 +112,78 @@ namespace k2h {
 #define K2H_X_PAIR_LAST(LO, HI, PAIR)                                                                      \
   K2H_X_SMEAR2(LO, HI, PAIR) K2H_X_WORD(LO, "v54") K2H_X_STEP(HI, "v58", 0) K2H_X_STEP(HI, "v58", 1)        \
       K2H_X_STEP(HI, "v58", 2) "v_mov_b32 v60, v48\n\tv_mov_b32 v61, v49\n\t" K2H_X_STEP(HI, "v58", 3)
+
+// The chunk helpers bind the state to v48/v49, the zero half of the addend pair to v50
+// and the chunk words to v[40:43] (v[44:47] for the second chunk) through physical-
+// register operand constraints ("{vN}"), so the allocator keeps the state in place from
+// one statement to the next (no copies in or out of the window) and the words sit in
+// adjacent pairs for the 64-bit-shift sign smear (K2H_X_SMEAR2 below).
+#define K2H_P_PAIR(LO, HI, PAIR) K2H_X_PAIR(LO, HI, PAIR)
+#define K2H_P_CLOBBERS "v51", "v52", "v53", "v54", "v56", "v57", "v58", "vcc", "memory"
+
+// 16 bytes (one uint4 chunk) into the state; BANK 1 takes the chunk in v[44:47]
+// instead of v[40:43], so a loop that alternates banks (ping-pong) needs no copies.
+template <int BANK = 0>
+__device__ __forceinline__ void fnv_chunk16(uint32_t& lo, uint32_t& hi, uint4 c) {
+  if constexpr (BANK == 0) {
+    asm(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_P_PAIR("v42", "v43", "v[42:43]")
+        : "+{v48}"(lo), "+{v49}"(hi)
+        : "{v40}"(c.x), "{v41}"(c.y), "{v42}"(c.z), "{v43}"(c.w), "{v50}"(0u), [p] "s"(kPrimeLo),
+          [sel] "s"(kSmearSel)
+        : K2H_P_CLOBBERS);
+  } else {
+    asm(K2H_P_PAIR("v44", "v45", "v[44:45]") K2H_P_PAIR("v46", "v47", "v[46:47]")
+        : "+{v48}"(lo), "+{v49}"(hi)
+        : "{v44}"(c.x), "{v45}"(c.y), "{v46}"(c.z), "{v47}"(c.w), "{v50}"(0u), [p] "s"(kPrimeLo),
+          [sel] "s"(kSmearSel)
+        : K2H_P_CLOBBERS);
+  }
+}
+
+// 32 bytes (two chunks), one statement.
+__device__ __forceinline__ void fnv_chunk32(uint32_t& lo, uint32_t& hi, uint4 a, uint4 b) {
+  asm(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_P_PAIR("v42", "v43", "v[42:43]")
+          K2H_P_PAIR("v44", "v45", "v[44:45]") K2H_P_PAIR("v46", "v47", "v[46:47]")
+      : "+{v48}"(lo), "+{v49}"(hi)
+      : "{v40}"(a.x), "{v41}"(a.y), "{v42}"(a.z), "{v43}"(a.w), "{v44}"(b.x), "{v45}"(b.y), "{v46}"(b.z),
+        "{v47}"(b.w), "{v50}"(0u), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+      : K2H_P_CLOBBERS);
+}
+
+// Last 16-byte chunk of a key: also returns the state before the final byte
+// (the reference's second hash, lib/k2hashfunc.cc:83-85).
+__device__ __forceinline__ void fnv_chunk16_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4 c) {
+  asm(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_X_PAIR_LAST("v42", "v43", "v[42:43]")
+      : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2)
+      : "{v40}"(c.x), "{v41}"(c.y), "{v42}"(c.z), "{v43}"(c.w), "{v50}"(0u), [p] "s"(kPrimeLo),
+        [sel] "s"(kSmearSel)
+      : K2H_P_CLOBBERS);
+}
+
+__device__ __forceinline__ void fnv_chunk32_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4 a,
+                                                 uint4 b) {
+  asm(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_P_PAIR("v42", "v43", "v[42:43]")
+          K2H_P_PAIR("v44", "v45", "v[44:45]") K2H_X_PAIR_LAST("v46", "v47", "v[46:47]")
+      : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2)
+      : "{v40}"(a.x), "{v41}"(a.y), "{v42}"(a.z), "{v43}"(a.w), "{v44}"(b.x), "{v45}"(b.y), "{v46}"(b.z),
+        "{v47}"(b.w), "{v50}"(0u), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+      : K2H_P_CLOBBERS);
+}
+
+}  // namespace k2h
+
+// ---------------------------------------------------------------------------
+// Whole-key statement for 32-byte keys (fixed32 fast path): the two 16-byte loads, all
+// 32 byte steps and the store in ONE asm statement over explicit registers, so that
+//  - each pair of words gets its sign smear from one 64-bit shift + two v_perm_b32
+//    (3 slow-issue ops per 8 bytes instead of 4), which needs the words in adjacent
+//    registers -- something operand constraints cannot express;
+//  - no moves in or out of the register window.
+// Register window: v[40:47] key words, v48/v49 state, v50 = 0, v51 t, v52 x_lo,
+// v53 m, v54/v58 smears, v[56:57] shifted pair, v[60:61] second-hash snapshot.
+// ---------------------------------------------------------------------------
+namespace k2h {
+
 #define K2H_X_HEAD                                                     \
   "global_load_dwordx4 v[40:43], %[src], off nt\n\t"                   \
   "global_load_dwordx4 v[44:47], %[src], off offset:16 nt\n\t"         \

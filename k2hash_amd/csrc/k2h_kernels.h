@@ -27,6 +27,8 @@ enum {
   kVariantCsrSingle = 13,      // csr staged: wave-uniform asm run over common chunks (lower VALU count,
                                // more dependency stalls at 2 waves/SIMD: slower, kept for A/B)
   kVariantCsrPairs = 14,       // csr staged: two chunks per asm statement (no uniform asm run)
+  kVariantCsrProf = 15,        // csr staged, diagnostics: h2 receives per-tile phase stamps
+                               // (16 words per 512-key tile, tools/csr_phases.py), not hashes
 };
 
 // S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).

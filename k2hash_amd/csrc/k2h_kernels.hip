@@ -329,6 +329,10 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
     }
     return hipGetLastError();
   }
+  // Routing by key length (tools/fixed_sweep.py on MI355X, 512 MiB of keys per launch):
+  // up to 32 B the per-lane tail loop is fastest, below 128 B per-lane direct 16-byte
+  // loads, from 128 B on the cooperative line ring.
+  if (variant == kVariantAuto) variant = key_len <= 32 ? kVariantFixedTail : key_len < 128 ? kVariantDirect : 0;
   if (variant != kVariantFixedTail)
     return launch_fixed_long(keys, key_len, n, seed, h1, h2, variant == kVariantDirect, stream);
   if (h2) fnv_fixed_kernel<true><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)keys, key_len, n, seed, h1, h2);
@@ -389,7 +393,13 @@ hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, ui
   if (n == 0) return hipSuccess;
   if (variant == kVariantSimpleCsr || !bytes) return launch_csr_simple(bytes, offsets, n, seed, h1, h2, stream);
   return launch_csr_tile(bytes, offsets, n, seed, h1, h2,
-                         variant == kVariantDirect ? 1 : variant == kVariantCsrRing ? 2 : variant == kVariantCsrPairs ? 3 : variant == kVariantCsrSingle ? 4 : 0, stream);
+                         variant == kVariantDirect      ? 1
+                         : variant == kVariantCsrRing   ? 2
+                         : variant == kVariantCsrPairs  ? 3
+                         : variant == kVariantCsrSingle ? 4
+                         : variant == kVariantCsrProf   ? 5
+                                                        : 0,
+                         stream);
 }
 
 }  // namespace k2h
