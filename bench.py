@@ -40,8 +40,12 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--warm-ms", type=float, default=150.0,
+                   help="keep warming up (untimed) until at least this much GPU time has passed: the "
+                        "MI355X clock ramps over the first ~30 ms of back-to-back launches "
+                        "(tools/clock_ramp.py, profiles/r01_clock_ramp.txt)")
     p.add_argument("--config", default="fixed32", choices=sorted(CONFIGS))
     p.add_argument("--second", action="store_true", help="also emit the second hash (h2)")
     p.add_argument("--gather", action="store_true", help="also time the RCCL gather of hashes (N>1)")
@@ -139,6 +143,13 @@ def main():
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
+    w0 = time.perf_counter()
+    extra = 0
+    while (time.perf_counter() - w0) * 1e3 < args.warm_ms:
+        for i in range(20):
+            step(i)
+        extra += 20
+        torch.cuda.synchronize()
     # One event pair around the K back-to-back launches on the stream they run on:
     # kernel time per launch = (end - start) / K (inter-kernel gaps included, ~1-2 us).
     e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -200,6 +211,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_extra_for_clock_ramp": extra,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "weak",
