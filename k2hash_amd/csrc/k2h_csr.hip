@@ -224,6 +224,7 @@ __device__ __forceinline__ void lds_hash(bool valid, uint64_t s, uint64_t e, uin
   uint32_t p = (uint32_t)(16u * k - len);
   // idle / empty-key lanes walk from the stage start (harmless reads, result discarded)
   const uint8_t* cp = k ? lds + (int64_t)(e - 16ull * k - tile_base) : lds;
+  if constexpr (WALK == 3) cp = (const uint8_t*)((uintptr_t)cp & ~(uintptr_t)15);  // timing probe: aligned reads
   uint64_t st = spad[p & 15u];
   uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2 = lo, hi2 = hi;
   // chunk j of the key is at cp + 16 j; body chunks 0..k-2, then the last chunk k-1
@@ -299,7 +300,10 @@ __device__ __forceinline__ uint32_t len_bin(uint64_t len) {
 // ---------------------------------------------------------------------------
 // CSR: one 256-thread block per tile of 512 keys.
 // ---------------------------------------------------------------------------
-enum { kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5 };
+enum {
+  kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
+  kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9
+};
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
 // wall clock per block at the phase boundaries, and each wave's finish time.
@@ -436,6 +440,116 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
 }
 
 // ---------------------------------------------------------------------------
+// CSR, lean staged tiles: TK keys per block of NW waves, the tile's bytes DMA'd into
+// an LDS stage of STAGE_KIB KiB with no line-ring union, so that several blocks fit a
+// CU (4 x 256-key tiles at 36 KiB: four tiles in flight per CU, one loading / sorting
+// while the others hash -- the 512-key kernel above fits two, and a tile spends about
+// half its life in latency-bound load / sort / DMA phases, tools/csr_phases.py).
+// Oversize tiles (span > stage) hash with per-lane direct loads.  Length classes are
+// 128 bins (exact chunk counts below 96).  Wave w of block b takes sorted groups
+// starting from (w + b) mod NW, snaking, so short and long groups spread over SIMDs.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t len_bin128(uint64_t len) {
+  if (len == 0) return 0;
+  uint64_t k = (len + 15) >> 4;
+  if (k < 96) return (uint32_t)k;
+  uint32_t lg = 63u - (uint32_t)__clzll((long long)k);  // >= 6
+  uint32_t b = 96u + (lg - 6u) * 4u + (uint32_t)((k >> (lg - 2u)) & 3u);
+  return b < 128u ? b : 127u;
+}
+
+template <bool H2, int TK, int NW, int STAGE_KIB, int WALK = 1>
+__global__ __launch_bounds__(NW * 64) void fnv_csr_lean_kernel(const uint8_t* __restrict__ bytes,
+                                                               const uint64_t* __restrict__ offsets, uint64_t n,
+                                                               SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                               uint64_t* __restrict__ h2) {
+  constexpr int NT = NW * 64;
+  constexpr int NB = 128;
+  constexpr uint32_t kStage = STAGE_KIB * 1024u;
+  static_assert(NT >= NB, "one thread per length class in the scan");
+  __shared__ uint64_t s_off[TK + 1];
+  __shared__ uint16_t s_order[TK];
+  __shared__ uint32_t s_hist[NB];
+  __shared__ uint32_t s_wsum[NW];
+  __shared__ uint64_t s_spad[16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[16 + kStage];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+  const uint64_t t0 = (uint64_t)blockIdx.x * TK;
+  const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
+  const uint8_t* lo_bound = bytes + offsets[0];
+
+  if (tid < 16) s_spad[tid] = spad_tab.v[tid];
+  for (uint32_t k = tid; k <= cnt; k += NT) s_off[k] = offsets[t0 + k];
+  if (tid < NB) s_hist[tid] = 0;
+  __syncthreads();
+
+  const uint64_t span_lo = ((uint64_t)(uintptr_t)bytes + s_off[0]) & ~15ull;
+  const uint64_t span_hi = (uint64_t)(uintptr_t)bytes + s_off[cnt];
+  const bool staged = span_hi - span_lo <= (uint64_t)kStage;
+  if (staged) {
+    const uint32_t npieces = s_off[cnt] > s_off[0] ? (uint32_t)((span_hi - span_lo + 1023) >> 10) : 0u;
+    for (uint32_t c = wave; c < npieces; c += NW) {
+      uint64_t src = span_lo + 1024ull * c + 16u * lane;
+      if (src >= span_hi) src = span_lo;
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(uintptr_t)src,
+                                       (__attribute__((address_space(3))) void*)(s_stage + 16 + 1024u * c), 16, 0, 0);
+    }
+  }
+  constexpr int KPT = (TK + NT - 1) / NT;
+  uint32_t bins[KPT];
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    uint32_t k = tid + NT * j;
+    if (k < cnt) {
+      bins[j] = len_bin128(s_off[k + 1] - s_off[k]);
+      atomicAdd(&s_hist[bins[j]], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t v = tid < NB ? s_hist[tid] : 0u, incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  __syncthreads();
+  uint32_t base = 0;
+  for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
+  if (tid < NB) s_hist[tid] = base + incl - v;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < KPT; ++j) {
+    uint32_t k = tid + NT * j;
+    if (k < cnt) s_order[atomicAdd(&s_hist[bins[j]], 1u)] = (uint16_t)k;
+  }
+  if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const uint32_t ngroups = (cnt + 63u) >> 6;
+  const uint32_t wr = (wave + blockIdx.x) % NW;
+  for (uint32_t it = 0; it * NW < ngroups; ++it) {
+    uint32_t g = it * NW + ((it & 1) ? NW - 1 - wr : wr);
+    if (g >= ngroups) continue;
+    uint32_t idx = g * 64u + lane;
+    bool valid = idx < cnt;
+    uint32_t k = s_order[valid ? idx : cnt - 1];
+    uint64_t r1 = 0, r2 = 0;
+    if (staged) {
+      lds_hash<WALK>(valid, (uint64_t)(uintptr_t)bytes + s_off[k], (uint64_t)(uintptr_t)bytes + s_off[k + 1], span_lo,
+                     s_stage + 16, s_spad, r1, r2);
+    } else if (valid) {
+      hash_key(bytes + s_off[k], bytes + s_off[k + 1], lo_bound, s_spad, r1, r2);
+    }
+    if (valid) {
+      h1[t0 + k] = r1;
+      if constexpr (H2) h2[t0 + k] = r2;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Fixed-length keys other than the 32-byte fast path (e.g. BASELINE config 5,
 // 4 KiB): one lane per key, the same chunk walker, uniform trip count.
 // ---------------------------------------------------------------------------
@@ -495,6 +609,27 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
       if (!h2) return hipErrorInvalidValue;
       fnv_csr_tile_kernel<false, kModeStagedProf><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2);
       break;
+    case kModeLean256: {
+      unsigned gl = (unsigned)((n + 255) / 256);
+      if (h2) fnv_csr_lean_kernel<true, 256, 4, 36><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2);
+      else fnv_csr_lean_kernel<false, 256, 4, 36><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr);
+      break;
+    }
+    case kModeLeanAlignProbe: {  // timing probe only: wrong hashes
+      unsigned gl = (unsigned)((n + 255) / 256);
+      fnv_csr_lean_kernel<false, 256, 4, 36, 3><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr);
+      break;
+    }
+    case kModeLean512x8: {
+      if (h2) fnv_csr_lean_kernel<true, 512, 8, 72><<<g, 512, 0, stream>>>(b, offsets, n, t, h1, h2);
+      else fnv_csr_lean_kernel<false, 512, 8, 72><<<g, 512, 0, stream>>>(b, offsets, n, t, h1, nullptr);
+      break;
+    }
+    case kModeLean512x4: {
+      if (h2) fnv_csr_lean_kernel<true, 512, 4, 72><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2);
+      else fnv_csr_lean_kernel<false, 512, 4, 72><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr);
+      break;
+    }
     default: K2H_CSR_LAUNCH(kModeStaged) break;
   }
 #undef K2H_CSR_LAUNCH

@@ -29,6 +29,13 @@ enum {
   kVariantCsrPairs = 14,       // csr staged: two chunks per asm statement (no uniform asm run)
   kVariantCsrProf = 15,        // csr staged, diagnostics: h2 receives per-tile phase stamps
                                // (16 words per 512-key tile, tools/csr_phases.py), not hashes
+  kVariantFixed32Ring2 = 16,   // fixed32: persistent one-wave blocks, LDS-DMA ring of 2 tiles
+  kVariantFixed32Ring3 = 17,   // fixed32: ... ring of 3 tiles (2 in flight while hashing)
+  kVariantFixed32Ring4 = 18,   // fixed32: ... ring of 4 tiles
+  kVariantCsrLean256 = 19,     // csr: 256-key tiles, 4 waves, 36 KiB stage, 4 blocks/CU, no ring union
+  kVariantCsrLean512x8 = 20,   // csr: 512-key tiles, 8 waves (one group each), 72 KiB stage
+  kVariantCsrLean512x4 = 21,   // csr: 512-key tiles, 4 waves, 72 KiB stage (the default kernel without the ring)
+  kVariantCsrAlignProbe = 22,  // csr timing probe (WRONG hashes): lean256 with 16-aligned LDS chunk reads
 };
 
 // S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).

@@ -262,6 +262,101 @@ __global__ __launch_bounds__(256) void fnv_fixed32_kpt_kernel(const uint4* __res
   }
 }
 
+// ---------------------------------------------------------------------------
+// fixed32, LDS-DMA ring: one-wave blocks, persistent.  Wave w hashes tiles of 64 keys
+// (2 KiB) w, w + W, w + 2W, ... and streams them through a private ring of S LDS slots
+// with global_load_lds_dwordx4 (two fully coalesced 1 KiB pieces per tile, no VGPRs
+// held), so each wave keeps S-1 tiles in flight while it hashes the current one --
+// the flat kernel holds at most one key per lane in flight and only while it waits.
+// Ordering: loads, LDS-DMA and stores share the in-order vmcnt counter
+// (MI355X_MICROARCH.md, s_waitcnt), and every iteration issues exactly two DMA pieces
+// (a dummy re-read of one line past the wave's last tile), so the wait that retires
+// tile j is vmcnt(2(S-1) + min(j, S-1) * stores per tile).
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void lds_read32(uint4& a, uint4& b, uint32_t addr) {
+  asm volatile(
+      "ds_read_b128 %0, %2\n\t"
+      "ds_read_b128 %1, %2 offset:16\n\t"
+      "s_waitcnt lgkmcnt(0)"
+      : "=v"(a), "=v"(b)
+      : "v"(addr)
+      : "memory");
+}
+
+template <bool H2, int S>
+__global__ __launch_bounds__(64) void fnv_fixed32_ring_kernel(const uint8_t* __restrict__ keys, uint64_t n,
+                                                              uint64_t seed, uint64_t* __restrict__ h1,
+                                                              uint64_t* __restrict__ h2) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[S][2048];
+  constexpr int kSt = H2 ? 2 : 1;  // stores per tile
+  const uint32_t lane = threadIdx.x;
+  const uint64_t ntiles = (n + 63) / 64;
+  const uint64_t W = gridDim.x;
+  const uint64_t t0 = blockIdx.x;
+  if (t0 >= ntiles) return;
+  const uint64_t m = (ntiles - t0 + W - 1) / W;  // tiles of this wave
+  const uint64_t last_chunk = 2 * n - 1;          // 16-byte pieces of the key buffer
+  auto issue = [&](uint64_t j) {
+    uint32_t slot = (uint32_t)(j % S);
+    uint64_t c0, c1;
+    if (j < m) {
+      uint64_t t = t0 + j * W;
+      c0 = t * 128 + lane;
+      c1 = c0 + 64;
+      c0 = c0 > last_chunk ? last_chunk : c0;
+      c1 = c1 > last_chunk ? last_chunk : c1;
+    } else {  // dummy: keeps the per-iteration vmcnt arithmetic uniform
+      c0 = c1 = t0 * 128;
+    }
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(uintptr_t)(keys + 16 * c0),
+                                     (__attribute__((address_space(3))) void*)&ring[slot][0], 16, 0, 0);
+    __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(uintptr_t)(keys + 16 * c1),
+                                     (__attribute__((address_space(3))) void*)&ring[slot][1024], 16, 0, 0);
+  };
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) issue(s);
+  for (uint64_t j = 0; j < m; ++j) {
+    issue(j + S - 1);
+    if (j >= S - 1) {
+      wait_vmcnt<2 * (S - 1) + (S - 1) * kSt>();
+    } else if constexpr (S >= 3) {
+      if (j == 0) wait_vmcnt<2 * (S - 1)>();
+      else if (j == 1) wait_vmcnt<2 * (S - 1) + kSt>();
+      else if constexpr (S >= 4) {
+        if (j == 2) wait_vmcnt<2 * (S - 1) + 2 * kSt>();
+        else wait_vmcnt<0>();
+      } else {
+        wait_vmcnt<0>();
+      }
+    } else {
+      wait_vmcnt<2 * (S - 1)>();
+    }
+    // the LDS reads are asm: hipcc would otherwise put a vmcnt(0) in front of any
+    // ds_read that may alias a pending LDS-DMA, draining the whole ring every tile
+    uint4 a, b;
+    lds_read32(a, b, (uint32_t)(uintptr_t)&ring[j % S][32u * lane]);
+    uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2, hi2;
+    uint64_t i = (t0 + j * W) * 64 + lane;
+    if constexpr (H2) {
+      fnv_chunk32_last(lo, hi, lo2, hi2, a, b);
+    } else {
+      fnv_chunk32(lo, hi, a, b);
+    }
+    // lane 0 of every tile of this wave is a real key (t < ntiles), so the store
+    // instruction is always issued and the per-iteration vmcnt arithmetic holds
+    if (i < n) {
+      st_nt(h1 + i, pack(lo, hi));
+      if constexpr (H2) st_nt(h2 + i, pack(lo2, hi2));
+    }
+  }
+  wait_vmcnt<0>();
+}
+
 static unsigned persist_grid(uint64_t units_of_256) {
   static int cus = 0;
   if (!cus) {
@@ -272,6 +367,28 @@ static unsigned persist_grid(uint64_t units_of_256) {
   }
   uint64_t g = (uint64_t)cus * 8;  // 8 x 256-thread blocks = 32 waves per CU
   return (unsigned)(units_of_256 < g ? units_of_256 : g);
+}
+
+// Resident one-wave blocks of the ring kernel per CU (occupancy query, LDS-bound), times
+// the CU count; never more blocks than tiles.
+static unsigned ring_grid(int variant, bool h2, uint64_t ntiles) {
+  static int cache[3][2] = {};
+  int v = variant == kVariantFixed32Ring2 ? 0 : variant == kVariantFixed32Ring3 ? 1 : 2;
+  int& per_cu = cache[v][h2];
+  if (!per_cu) {
+    const void* f = nullptr;
+    switch (v) {
+      case 0: f = h2 ? (const void*)fnv_fixed32_ring_kernel<true, 2> : (const void*)fnv_fixed32_ring_kernel<false, 2>; break;
+      case 1: f = h2 ? (const void*)fnv_fixed32_ring_kernel<true, 3> : (const void*)fnv_fixed32_ring_kernel<false, 3>; break;
+      default: f = h2 ? (const void*)fnv_fixed32_ring_kernel<true, 4> : (const void*)fnv_fixed32_ring_kernel<false, 4>; break;
+    }
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, f, 64, 0) != hipSuccess || per_cu <= 0) per_cu = 16;
+  }
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    cus = 256;
+  uint64_t g = (uint64_t)cus * (uint64_t)per_cu;
+  return (unsigned)(ntiles < g ? ntiles : g);
 }
 
 hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
@@ -318,6 +435,19 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
         unsigned g = persist_grid((n + 255) / 256);
         if (h2) fnv_fixed32_lds_kernel<true><<<g, 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_lds_kernel<false><<<g, 256, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
+      case kVariantFixed32Ring3:
+      case kVariantFixed32Ring4:
+      case kVariantFixed32Ring2: {
+        unsigned g = ring_grid(variant, h2 != nullptr, (n + 63) / 64);
+#define K2H_RING(SS)                                                                                      \
+  if (h2) fnv_fixed32_ring_kernel<true, SS><<<g, 64, 0, stream>>>((const uint8_t*)keys, n, seed, h1, h2); \
+  else fnv_fixed32_ring_kernel<false, SS><<<g, 64, 0, stream>>>((const uint8_t*)keys, n, seed, h1, nullptr);
+        if (variant == kVariantFixed32Ring2) { K2H_RING(2) }
+        else if (variant == kVariantFixed32Ring4) { K2H_RING(4) }
+        else { K2H_RING(3) }
+#undef K2H_RING
         break;
       }
       default: {  // kVariantFixed32Persist
@@ -398,6 +528,10 @@ hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, ui
                          : variant == kVariantCsrPairs  ? 3
                          : variant == kVariantCsrSingle ? 4
                          : variant == kVariantCsrProf   ? 5
+                         : variant == kVariantCsrLean256  ? 6
+                         : variant == kVariantCsrLean512x8 ? 7
+                         : variant == kVariantCsrLean512x4 ? 8
+                         : variant == kVariantCsrAlignProbe ? 9
                                                         : 0,
                          stream);
 }

@@ -16,7 +16,8 @@ from k2hash_amd import batch
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12]
+VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12, 16, 17, 18]
+CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21]
 
 
 def dev_u8(torch, arr, device, pad_front=0):
@@ -53,6 +54,24 @@ def test_fixed32_vs_oracle(cuda, oracle, n, variant):
     assert np.array_equal(host_u64(g1), r1)
 
 
+@pytest.mark.parametrize("variant", [0, 5, 6, 16, 17, 18])
+@pytest.mark.parametrize("n", [(1 << 21) + 17, 3 << 20])
+def test_fixed32_persistent_many_tiles(cuda, oracle, n, variant):
+    """Persistent / ring kernels at sizes where every wave walks many tiles (the
+    small cases above give most waves a single tile)."""
+    import torch
+    batch.set_variant(variant)
+    data = oracle.gen_bytes(32 * n, byte_off=32 * 777)
+    r1, r2 = oracle.hash_fixed(data, 32)
+    keys = dev_u8(torch, data, cuda)
+    h1, h2 = k2hash_amd.hash_fixed(keys, 32, second=True)
+    g1, _ = k2hash_amd.hash_fixed(keys, 32, second=False)
+    torch.cuda.synchronize()
+    assert np.array_equal(host_u64(h1), r1)
+    assert np.array_equal(host_u64(h2), r2)
+    assert np.array_equal(host_u64(g1), r1)
+
+
 @pytest.mark.parametrize("key_len", list(range(1, 72)) + [95, 96, 97, 127, 128, 129, 255, 256, 257, 1000, 4095, 4096])
 def test_fixed_any_length_vs_oracle(cuda, oracle, key_len):
     import torch
@@ -74,7 +93,7 @@ def _csr(keys):
     return data, off
 
 
-@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("variant", CSR_VARIANTS)
 def test_golden_vectors_csr(cuda, vectors, variant):
     import torch
     batch.set_variant(variant)
@@ -89,7 +108,7 @@ def test_golden_vectors_csr(cuda, vectors, variant):
             assert (int(a[i]), int(b[i])) == (u64(v["h1"]), u64(v["h2"])), (field, v["tag"], v["len"])
 
 
-@pytest.mark.parametrize("variant", [0, 3])
+@pytest.mark.parametrize("variant", CSR_VARIANTS)
 @pytest.mark.parametrize("lens", ["mixed", "zeros", "long", "uniform"])
 def test_csr_vs_oracle(cuda, oracle, lens, variant):
     import torch
@@ -199,9 +218,11 @@ def test_full_size_fixed_digest(cuda, oracle, digests, name):
     assert torch.equal(g1, h1)
 
 
+@pytest.mark.parametrize("variant", [0, 19, 20, 21])
 @pytest.mark.parametrize("name", ["csr_8_256_64M", "csr_8_256_64K"])
-def test_full_size_csr_digest(cuda, oracle, digests, name):
+def test_full_size_csr_digest(cuda, oracle, digests, name, variant):
     import torch
+    batch.set_variant(variant)
     cfg = digests[name]
     off = batch.synth_offsets(cfg["n"], cuda, cfg["min_len"], cfg["max_len"])
     data = batch.synth_bytes(int(off[-1].item()), cuda)
