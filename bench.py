@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--config", default="fixed32", choices=sorted(CONFIGS))
     p.add_argument("--second", action="store_true", help="also emit the second hash (h2)")
     p.add_argument("--gather", action="store_true", help="also time the RCCL gather of hashes (N>1)")
+    p.add_argument("--index", action="store_true",
+                   help="fused bucket-index epilogue (kindex + ckindex outputs, SURVEY 8f rank 1) with a "
+                        "2^28-slot table: cur_mask 0x0FFFFFFF, collision_mask 0xF")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--variant", type=int, default=0, help="kernel variant (A/B knob, 0 = auto)")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
@@ -129,13 +132,30 @@ def main():
             algo_bytes = max(algo_bytes, int(off[-1].item()) + 8 * n + 8 * (n + 1))
     if args.second:
         algo_bytes += 8 * n
+    if args.index:
+        algo_bytes += 16 * n  # kindex + ckindex writes
     outs = [(torch.empty(n, dtype=torch.int64, device=dev),
              torch.empty(n, dtype=torch.int64, device=dev) if args.second else None) for _ in range(2)]
+    idx = [(torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
+           for _ in range(2)] if args.index else None
     torch.cuda.synchronize()
+    lib = k2hash_amd._native.batch_lib()
+    CUR_MASK, CMASK = (1 << 28) - 1, 0xF
 
     def step(i):
         keys, off = sets[i & 1]
-        if kind == "fixed":
+        if args.index:
+            import ctypes
+            h1, h2 = outs[i & 1]
+            k, c = idx[i & 1]
+            p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+            s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+            if kind == "fixed":
+                rc = lib.k2h_amd_hash_fixed_index(p(keys), shape, n, p(h1), p(h2), 0, CUR_MASK, CMASK, p(k), p(c), s)
+            else:
+                rc = lib.k2h_amd_hash_csr_index(p(keys), p(off), n, p(h1), p(h2), 0, CUR_MASK, CMASK, p(k), p(c), s)
+            k2hash_amd._native.check(rc)
+        elif kind == "fixed":
             k2hash_amd.hash_fixed(keys, shape, second=args.second, out=outs[i & 1])
         else:
             k2hash_amd.hash_csr(keys, off, second=args.second, out=outs[i & 1])
@@ -199,13 +219,14 @@ def main():
     if rank == 0:
         achieved = algo_bytes / kern_avg_s / 1e9
         traffic = None
-        prof = ROOT / "profiles" / f"traffic_{args.config}.json"
+        prof = ROOT / "profiles" / f"traffic_{args.config}{'_index' if args.index else ''}{'_h2' if args.second else ''}.json"
         if prof.exists():
             traffic = json.loads(prof.read_text()).get("hbm_bytes_per_launch")
         key_bytes = n * (shape if kind == "fixed" else (shape[0] + shape[1]) / 2)
         line = {
             "metric": "key hashes/sec + GiB/s (device-resident), batched 32B keys, 1 MI355X"
-            if args.config == "fixed32" else f"key hashes/sec (device-resident), {desc}",
+            if args.config == "fixed32" and not (args.index or args.second)
+            else f"key hashes{' + bucket indices' if args.index else ''}/sec (device-resident), {desc}",
             "value": value,
             "unit": "key hashes/s",
             "n_gpus": world,
@@ -220,7 +241,8 @@ def main():
             "data": "synthetic (splitmix64 counter stream, generated on device; SURVEY.md 8d spec in DESIGN.md)",
             "config": {"workload": desc, "keys_per_gpu": n,
                        "key_len": shape if kind == "fixed" else list(shape),
-                       "second_hash": bool(args.second), "parallelism": f"shard{world}",
+                       "second_hash": bool(args.second), "bucket_index": bool(args.index),
+                       "parallelism": f"shard{world}",
                        "variant": args.variant},
             "key_gib_per_s": value * (key_bytes / n) / 2**30,
             "kernel_ms": kern_avg_s * 1e3,

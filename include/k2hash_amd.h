@@ -95,6 +95,37 @@ int k2h_amd_hash_fixed_host(const void* keys, uint64_t key_len, uint64_t n, uint
 int k2h_amd_hash_csr_host(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1, uint64_t* h2,
                           uint32_t flags, int device);
 
+/* ---------------------------------------------------------------------------
+ * 3. Bucket-index epilogue (where each key lands in a k2hash table).
+ *
+ * For table masks (cur_mask, collision_mask) -- K2HSHM header fields, e.g. the
+ * defaults 0xFF / 0xF of K2HShm::DEFAULT_MASK_BITCOUNT / DEFAULT_COLLISION_MASK_BITCOUNT
+ * (lib/k2hshm.h:132-133) -- computes per hash h the stateless part of
+ * K2HShm::GetKIndexPos (lib/k2hshm.cc:810-833, MakeMask / GetMaskBitCount at :78-90)
+ * and the collision slot of K2HShm::GetCKIndex (lib/k2hshm.cc:1093):
+ *   shifted       = h >> GetMaskBitCount(collision_mask)   (count taken mod 64)
+ *   KIPtrArrayPos = GetMaskBitCount(shifted & cur_mask)
+ *   KIArrayPos    = shifted & MakeMask(KIPtrArrayPos ? KIPtrArrayPos - 1 : 0)
+ *   kindex[i]     = KIPtrArrayPos << 58 | KIArrayPos     (K2H_AMD_KINDEX_* below)
+ *   ckindex[i]    = h & collision_mask
+ * i.e. &key_index_area[KIPtrArrayPos][KIArrayPos] (CVT_ABS_PKINDEX, lib/k2hshm.cc:50)
+ * and &ckey_list[ckindex].  The table-state part of GetKIndex (walking cur_mask down
+ * past unassigned K_INDEX entries, lib/k2hshm.cc:882-907) stays with the caller.
+ * kindex and ckindex may each be NULL; cur_mask must fit 58 bits when kindex is wanted.
+ * The fused forms hash and index in one pass (the index costs no extra key read).
+ * ------------------------------------------------------------------------- */
+#define K2H_AMD_KINDEX_POS(v) ((uint64_t)(v) >> 58)                     /* KIPtrArrayPos */
+#define K2H_AMD_KINDEX_ARR(v) ((uint64_t)(v) & ((1ull << 58) - 1ull))  /* KIArrayPos */
+
+int k2h_amd_bucket_index(const uint64_t* h1, uint64_t n, uint64_t cur_mask, uint64_t collision_mask,
+                         uint64_t* kindex, uint64_t* ckindex, void* stream);
+int k2h_amd_hash_fixed_index(const void* keys, uint64_t key_len, uint64_t n, uint64_t* h1, uint64_t* h2,
+                             uint32_t flags, uint64_t cur_mask, uint64_t collision_mask, uint64_t* kindex,
+                             uint64_t* ckindex, void* stream);
+int k2h_amd_hash_csr_index(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1, uint64_t* h2,
+                           uint32_t flags, uint64_t cur_mask, uint64_t collision_mask, uint64_t* kindex,
+                           uint64_t* ckindex, void* stream);
+
 /* Identity / diagnostics. */
 const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */
 const char* k2h_amd_strerror(int code); /* message for `code`, with the last HIP error if any */

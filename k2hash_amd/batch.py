@@ -89,6 +89,85 @@ def hash_csr(data, offsets, second: bool = False, std_fnv: bool = False, out: Op
     return h1, h2
 
 
+# ----------------------------------------------------------------------------
+# Bucket-index epilogue (include/k2hash_amd.h section 3; lib/k2hshm.cc:78-90,
+# 810-833, 1093): where each hash lands in a k2hash table with masks
+# (cur_mask, collision_mask).  kindex packs KIPtrArrayPos << 58 | KIArrayPos.
+# ----------------------------------------------------------------------------
+KINDEX_POS_SHIFT = 58
+
+
+def unpack_kindex(kindex):
+    """(KIPtrArrayPos, KIArrayPos) from packed kindex values (numpy uint64 or torch int64)."""
+    if isinstance(kindex, np.ndarray):
+        v = kindex.view(np.uint64)
+        return v >> np.uint64(KINDEX_POS_SHIFT), v & np.uint64((1 << KINDEX_POS_SHIFT) - 1)
+    pos = (kindex >> KINDEX_POS_SHIFT) & 0x3F
+    return pos, kindex & ((1 << KINDEX_POS_SHIFT) - 1)
+
+
+def _index_outs(torch, n, device, kindex, ckindex, out):
+    if out is not None:
+        return out
+    k = torch.empty(n, dtype=torch.int64, device=device) if kindex else None
+    c = torch.empty(n, dtype=torch.int64, device=device) if ckindex else None
+    return k, c
+
+
+def bucket_index(h1, cur_mask: int, collision_mask: int, kindex: bool = True, ckindex: bool = True,
+                 out=None, stream=None):
+    """Bucket positions of hashes already in device memory (int64 tensor)."""
+    torch = _torch()
+    _check_dev(h1, "h1", torch.int64)
+    n = h1.numel()
+    k, c = _index_outs(torch, n, h1.device, kindex, ckindex, out)
+    rc = _native.batch_lib().k2h_amd_bucket_index(
+        _dev_ptr(h1), n, cur_mask, collision_mask, _dev_ptr(k) if k is not None else None,
+        _dev_ptr(c) if c is not None else None, _stream_handle(stream))
+    _native.check(rc)
+    return k, c
+
+
+def hash_fixed_index(keys, key_len: int, cur_mask: int, collision_mask: int, second: bool = False,
+                     std_fnv: bool = False, kindex: bool = True, ckindex: bool = True, stream=None):
+    """hash_fixed + bucket index in one pass: returns (h1, h2, kindex, ckindex)."""
+    torch = _torch()
+    _check_dev(keys, "keys", torch.uint8)
+    if key_len <= 0:
+        raise ValueError("key_len must be positive")
+    n = keys.numel() // key_len
+    h1 = torch.empty(n, dtype=torch.int64, device=keys.device)
+    h2 = torch.empty(n, dtype=torch.int64, device=keys.device) if second else None
+    k, c = _index_outs(torch, n, keys.device, kindex, ckindex, None)
+    rc = _native.batch_lib().k2h_amd_hash_fixed_index(
+        _dev_ptr(keys), key_len, n, _dev_ptr(h1), _dev_ptr(h2) if h2 is not None else None,
+        FLAG_STD_FNV if std_fnv else 0, cur_mask, collision_mask, _dev_ptr(k) if k is not None else None,
+        _dev_ptr(c) if c is not None else None, _stream_handle(stream))
+    _native.check(rc)
+    return h1, h2, k, c
+
+
+def hash_csr_index(data, offsets, cur_mask: int, collision_mask: int, second: bool = False,
+                   std_fnv: bool = False, kindex: bool = True, ckindex: bool = True, stream=None):
+    """hash_csr + bucket index in one pass: returns (h1, h2, kindex, ckindex)."""
+    torch = _torch()
+    _check_dev(data, "data", torch.uint8)
+    _check_dev(offsets, "offsets", torch.int64)
+    n = offsets.numel() - 1
+    if n < 0:
+        raise ValueError("offsets must have n+1 entries")
+    h1 = torch.empty(n, dtype=torch.int64, device=data.device)
+    h2 = torch.empty(n, dtype=torch.int64, device=data.device) if second else None
+    k, c = _index_outs(torch, n, data.device, kindex, ckindex, None)
+    base = _dev_ptr(data) if data.numel() > 0 else ctypes.c_void_p(data.data_ptr() or 1)
+    rc = _native.batch_lib().k2h_amd_hash_csr_index(
+        base, _dev_ptr(offsets), n, _dev_ptr(h1), _dev_ptr(h2) if h2 is not None else None,
+        FLAG_STD_FNV if std_fnv else 0, cur_mask, collision_mask, _dev_ptr(k) if k is not None else None,
+        _dev_ptr(c) if c is not None else None, _stream_handle(stream))
+    _native.check(rc)
+    return h1, h2, k, c
+
+
 def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 

@@ -12,7 +12,14 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <mutex>
+#include <thread>
+#include <vector>
 
 #include "../../include/k2hash_amd.h"
 #include "k2h_kernels.h"
@@ -40,6 +47,92 @@ int fail(int code, const char* what, hipError_t e = hipSuccess) {
 
 uint64_t seed_for(uint32_t flags) {
   return (flags & K2H_AMD_FLAG_STD_FNV) ? k2h::kSeedStdValue : k2h::kSeedBuiltinValue;
+}
+
+// ---------------------------------------------------------------------------
+// Parallel host copies for the staging pipeline.  One core's memcpy into pinned memory
+// runs at ~16 GB/s on the MI355X hosts, a third of PCIe (57 GB/s measured,
+// tools/host_rate.py), so staging copies are split over a small worker pool.  The pool
+// is created on the first host-path call (never at library load) and re-created in a
+// forked child, whose copy of the pool has no threads.
+// ---------------------------------------------------------------------------
+class CopyPool {
+ public:
+  void copy(void* dst, const void* src, size_t len) {
+    if (len < (4u << 20) || nthreads() <= 1) {
+      memcpy(dst, src, len);
+      return;
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    ensure();
+    dst_ = (uint8_t*)dst;
+    src_ = (const uint8_t*)src;
+    len_ = len;
+    piece_ = std::max<size_t>(1u << 20, (len + 4 * (nworkers_ + 1) - 1) / (4 * (nworkers_ + 1)));
+    piece_ = (piece_ + 4095) & ~(size_t)4095;
+    next_.store(0);
+    busy_ = nworkers_;
+    ++gen_;
+    cv_.notify_all();
+    lk.unlock();
+    run();  // the caller copies too
+    lk.lock();
+    done_cv_.wait(lk, [&] { return busy_ == 0; });
+  }
+
+ private:
+  static int nthreads() {
+    static int n = [] {
+      const char* e = getenv("K2H_AMD_COPY_THREADS");
+      int v = e ? atoi(e) : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency() / 2));
+      return v < 1 ? 1 : v;
+    }();
+    return n;
+  }
+  void ensure() {
+    if (pid_ == getpid() && nworkers_) return;
+    // (re)start: in a forked child the parent's workers do not exist.  Workers are
+    // detached and the pool is never destroyed (see pool()), so process exit neither
+    // joins nor terminates them.
+    nworkers_ = 0;
+    pid_ = getpid();
+    gen_ = 0;
+    for (int i = 0; i < nthreads() - 1; ++i, ++nworkers_)
+      std::thread([this] {
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(mu_);
+        for (;;) {
+          cv_.wait(lk, [&] { return gen_ != seen; });
+          seen = gen_;
+          lk.unlock();
+          run();
+          lk.lock();
+          if (--busy_ == 0) done_cv_.notify_all();
+        }
+      }).detach();
+  }
+  void run() {
+    for (;;) {
+      size_t off = next_.fetch_add(piece_);
+      if (off >= len_) return;
+      memcpy(dst_ + off, src_ + off, std::min(piece_, len_ - off));
+    }
+  }
+  std::mutex mu_;
+  std::condition_variable cv_, done_cv_;
+  size_t nworkers_ = 0;
+  pid_t pid_ = 0;
+  uint64_t gen_ = 0;
+  size_t busy_ = 0;
+  uint8_t* dst_ = nullptr;
+  const uint8_t* src_ = nullptr;
+  size_t len_ = 0, piece_ = 0;
+  std::atomic<size_t> next_{0};
+};
+
+CopyPool& pool() {
+  static CopyPool* p = new CopyPool;  // never destroyed: detached workers may outlive statics
+  return *p;
 }
 
 // ---------------------------------------------------------------------------
@@ -113,8 +206,8 @@ int slot_drain(Slot& s, uint64_t* h1, uint64_t* h2) {
   hipError_t e = hipEventSynchronize(s.done);
   s.busy = false;
   if (e != hipSuccess) return fail(K2H_AMD_EHIP, "chunk completion", e);
-  memcpy(h1 + s.first, s.h_out, s.count * 8);
-  if (s.want_h2 && h2) memcpy(h2 + s.first, s.h_out + s.count, s.count * 8);
+  pool().copy(h1 + s.first, s.h_out, s.count * 8);
+  if (s.want_h2 && h2) pool().copy(h2 + s.first, s.h_out + s.count, s.count * 8);
   return K2H_AMD_OK;
 }
 
@@ -155,6 +248,70 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr(const void* bytes, c
   return K2H_AMD_OK;
 }
 
+}  // extern "C"
+
+namespace {
+int bucket_params(uint64_t cur_mask, uint64_t collision_mask, uint64_t* kindex, uint64_t* ckindex,
+                  k2h::BucketParams& bp) {
+  int bits = 0;
+  for (uint64_t m = cur_mask; m; m >>= 1) ++bits;  // GetMaskBitCount, lib/k2hshm.cc:85-90
+  if (kindex && bits > k2h::kKindexPosShift)
+    return fail(K2H_AMD_EINVAL, "cur_mask wider than 58 bits cannot be packed into kindex");
+  int cbits = 0;
+  for (uint64_t m = collision_mask; m; m >>= 1) ++cbits;
+  bp.cur_mask = cur_mask;
+  bp.collision_mask = collision_mask;
+  bp.cshift = (uint32_t)cbits;
+  bp.kindex = kindex;
+  bp.ckindex = ckindex;
+  return K2H_AMD_OK;
+}
+}  // namespace
+
+extern "C" {
+
+__attribute__((visibility("default"))) int k2h_amd_bucket_index(const uint64_t* h1, uint64_t n, uint64_t cur_mask,
+                                                                uint64_t collision_mask, uint64_t* kindex,
+                                                                uint64_t* ckindex, void* stream) {
+  if (n == 0 || (!kindex && !ckindex)) return K2H_AMD_OK;
+  if (!h1) return fail(K2H_AMD_EINVAL, "h1 is NULL");
+  k2h::BucketParams bp;
+  int rc = bucket_params(cur_mask, collision_mask, kindex, ckindex, bp);
+  if (rc) return rc;
+  hipError_t e = k2h::launch_bucket_index(h1, n, bp, (hipStream_t)stream);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_bucket_index", e);
+}
+
+__attribute__((visibility("default"))) int k2h_amd_hash_fixed_index(const void* keys, uint64_t key_len, uint64_t n,
+                                                                    uint64_t* h1, uint64_t* h2, uint32_t flags,
+                                                                    uint64_t cur_mask, uint64_t collision_mask,
+                                                                    uint64_t* kindex, uint64_t* ckindex,
+                                                                    void* stream) {
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1) return fail(K2H_AMD_EINVAL, "h1 is NULL");
+  if (key_len && n > UINT64_MAX / key_len) return fail(K2H_AMD_EINVAL, "n * key_len overflows");
+  k2h::BucketParams bp;
+  int rc = bucket_params(cur_mask, collision_mask, kindex, ckindex, bp);
+  if (rc) return rc;
+  hipError_t e =
+      k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream, &bp);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_fixed (index)", e);
+}
+
+__attribute__((visibility("default"))) int k2h_amd_hash_csr_index(const void* bytes, const uint64_t* offsets,
+                                                                  uint64_t n, uint64_t* h1, uint64_t* h2,
+                                                                  uint32_t flags, uint64_t cur_mask,
+                                                                  uint64_t collision_mask, uint64_t* kindex,
+                                                                  uint64_t* ckindex, void* stream) {
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1 || !offsets) return fail(K2H_AMD_EINVAL, "h1/offsets is NULL");
+  k2h::BucketParams bp;
+  int rc = bucket_params(cur_mask, collision_mask, kindex, ckindex, bp);
+  if (rc) return rc;
+  hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream, &bp);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_csr (index)", e);
+}
+
 __attribute__((visibility("default"))) int k2h_amd_hash_fixed_host(const void* keys, uint64_t key_len, uint64_t n,
                                                                    uint64_t* h1, uint64_t* h2, uint32_t flags,
                                                                    int device) {
@@ -180,7 +337,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed_host(const void* k
     Slot& s = c.slot[k];
     if ((rc = slot_drain(s, h1, h2))) return rc;
     if ((rc = slot_reserve(s, per * key_len, per))) return rc;
-    memcpy(s.h_in, src + first * key_len, cnt * key_len);
+    pool().copy(s.h_in, src + first * key_len, cnt * key_len);
     hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, cnt * key_len, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess)
       e = k2h::launch_fixed(s.d_in, key_len, cnt, seed_for(flags), s.d_out, h2 ? s.d_out + cnt : nullptr, variant(),
@@ -227,7 +384,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* byt
     Slot& s = c.slot[k];
     if ((rc = slot_drain(s, h1, h2))) return rc;
     if ((rc = slot_reserve(s, nb > kChunkBytes ? nb : kChunkBytes, kChunkKeysMax))) return rc;
-    memcpy(s.h_in, src + offsets[first], nb);
+    pool().copy(s.h_in, src + offsets[first], nb);
     for (uint64_t i = 0; i <= cnt; ++i) s.h_off[i] = offsets[first + i] - offsets[first];
     hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, nb, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice, s.stream);

@@ -312,11 +312,11 @@ enum {
     if (tid == 0) prof[(uint64_t)blockIdx.x * 16u + (SLOT)] = __builtin_amdgcn_s_memrealtime(); \
   }
 
-template <bool H2, int MODE>
+template <bool H2, int MODE, bool EPI = false>
 __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __restrict__ bytes,
                                                            const uint64_t* __restrict__ offsets, uint64_t n,
                                                            SpadTable spad_tab, uint64_t* __restrict__ h1,
-                                                           uint64_t* __restrict__ h2) {
+                                                           uint64_t* __restrict__ h2, BucketParams bp = {}) {
   __shared__ uint64_t s_off[kTileKeys + 1];
   __shared__ uint16_t s_order[kTileKeys];
   __shared__ uint32_t s_hist[kBins];
@@ -422,6 +422,7 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
     if (valid) {
       h1[t0 + k] = r1;
       if constexpr (H2) h2[t0 + k] = r2;
+      if constexpr (EPI) bucket_emit<false>(bp, t0 + k, r1);
     }
   }
   if constexpr (MODE == kModeStagedProf) {
@@ -553,10 +554,11 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_lean_kernel(const uint8_t* __
 // Fixed-length keys other than the 32-byte fast path (e.g. BASELINE config 5,
 // 4 KiB): one lane per key, the same chunk walker, uniform trip count.
 // ---------------------------------------------------------------------------
-template <bool H2, bool DIRECT>
+template <bool H2, bool DIRECT, bool EPI = false>
 __global__ __launch_bounds__(256) void fnv_fixed_long_kernel(const uint8_t* __restrict__ base, uint64_t key_len,
                                                              uint64_t n, SpadTable spad_tab,
-                                                             uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+                                                             uint64_t* __restrict__ h1, uint64_t* __restrict__ h2,
+                                                             BucketParams bp = {}) {
   __shared__ uint64_t s_spad[16];
   __shared__ Ring s_ring[DIRECT ? 1 : 4];
   if (threadIdx.x < 16) s_spad[threadIdx.x] = spad_tab.v[threadIdx.x];
@@ -576,6 +578,7 @@ __global__ __launch_bounds__(256) void fnv_fixed_long_kernel(const uint8_t* __re
   }
   __builtin_nontemporal_store(r1, h1 + i);
   if constexpr (H2) __builtin_nontemporal_store(r2, h2 + i);
+  if constexpr (EPI) bucket_emit(bp, i, r1);
 }
 
 // S_p = seed * P^-p mod 2^64, p = 0..15 (P = 1099511628211 is odd, so invertible).
@@ -593,10 +596,15 @@ SpadTable make_spad(uint64_t seed) {
 }
 
 hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
-                           uint64_t* h2, int mode, hipStream_t stream) {
+                           uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
   SpadTable t = make_spad(seed);
   unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
   const uint8_t* b = (const uint8_t*)bytes;
+  if (bp && mode == kModeStaged) {  // fused epilogue on the default kernel
+    if (h2) fnv_csr_tile_kernel<true, kModeStaged, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, *bp);
+    else fnv_csr_tile_kernel<false, kModeStaged, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, *bp);
+    return hipGetLastError();
+  }
 #define K2H_CSR_LAUNCH(M)                                                                      \
   if (h2) fnv_csr_tile_kernel<true, M><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2);       \
   else fnv_csr_tile_kernel<false, M><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr);
@@ -633,14 +641,20 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
     default: K2H_CSR_LAUNCH(kModeStaged) break;
   }
 #undef K2H_CSR_LAUNCH
+  if (bp) return launch_bucket_index(h1, n, *bp, stream);  // A/B modes: unfused epilogue
   return hipGetLastError();
 }
 
 hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
-                             uint64_t* h2, bool direct, hipStream_t stream) {
+                             uint64_t* h2, bool direct, hipStream_t stream, const BucketParams* bp) {
   SpadTable t = make_spad(seed);
   unsigned g = (unsigned)((n + 255) / 256);
   const uint8_t* k = (const uint8_t*)keys;
+  if (bp && !direct) {  // fused epilogue on the default (line ring) kernel
+    if (h2) fnv_fixed_long_kernel<true, false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2, *bp);
+    else fnv_fixed_long_kernel<false, false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr, *bp);
+    return hipGetLastError();
+  }
   if (direct) {
     if (h2) fnv_fixed_long_kernel<true, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2);
     else fnv_fixed_long_kernel<false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr);
@@ -648,6 +662,7 @@ hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uin
     if (h2) fnv_fixed_long_kernel<true, false><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2);
     else fnv_fixed_long_kernel<false, false><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr);
   }
+  if (bp) return launch_bucket_index(h1, n, *bp, stream);
   return hipGetLastError();
 }
 

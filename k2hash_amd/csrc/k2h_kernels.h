@@ -38,6 +38,50 @@ enum {
   kVariantCsrAlignProbe = 22,  // csr timing probe (WRONG hashes): lean256 with 16-aligned LDS chunk reads
 };
 
+// Bucket-index epilogue: where a hash lands in a k2hash table with
+// masks (cur_mask, collision_mask) -- the stateless part of K2HShm::GetKIndexPos
+// (lib/k2hshm.cc:810-833, with MakeMask / GetMaskBitCount at :78-90) and the collision
+// slot `hash & collision_mask` (lib/k2hshm.cc:1093).
+//   shifted       = hash >> bitlen(collision_mask)   (shift count taken mod 64, as the
+//                                                     x86-64 shr the reference compiles to)
+//   KIPtrArrayPos = bitlen(shifted & cur_mask)        (the reference's bitmask loop)
+//   KIArrayPos    = shifted & MakeMask(KIPtrArrayPos - 1)   (MakeMask(0) = 0)
+// kindex[i] packs KIPtrArrayPos << 58 | KIArrayPos (bitlen(cur_mask) <= 58 checked by the
+// ABI); ckindex[i] = hash & collision_mask.  Either output may be null.
+struct BucketParams {
+  uint64_t cur_mask = 0;
+  uint64_t collision_mask = 0;
+  uint32_t cshift = 0;
+  uint64_t* kindex = nullptr;
+  uint64_t* ckindex = nullptr;
+};
+constexpr int kKindexPosShift = 58;
+
+#ifdef __HIPCC__
+// NT: nontemporal stores, for kernels whose lanes write consecutive i (a wave fills
+// whole lines); kernels that write in a permuted order (CSR tiles, length-sorted) use
+// plain stores so that L2 merges the partial lines before they reach HBM.
+template <bool NT = true>
+__device__ __forceinline__ void bucket_emit(const BucketParams& bp, uint64_t i, uint64_t h) {
+  if (bp.kindex) {
+    uint64_t shifted = h >> (bp.cshift & 63u);
+    uint64_t tmp = shifted & bp.cur_mask;
+    uint64_t pos = tmp ? 64u - (uint64_t)__clzll((long long)tmp) : 0u;
+    uint64_t arr = pos ? shifted & ((1ull << (pos - 1)) - 1ull) : 0u;
+    uint64_t v = (pos << kKindexPosShift) | arr;
+    if constexpr (NT) __builtin_nontemporal_store(v, bp.kindex + i);
+    else bp.kindex[i] = v;
+  }
+  if (bp.ckindex) {
+    if constexpr (NT) __builtin_nontemporal_store(h & bp.collision_mask, bp.ckindex + i);
+    else bp.ckindex[i] = h & bp.collision_mask;
+  }
+}
+#endif
+
+// Standalone epilogue over hashes already in device memory.
+hipError_t launch_bucket_index(const uint64_t* h1, uint64_t n, const BucketParams& bp, hipStream_t stream);
+
 // S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).
 struct SpadTable {
   uint64_t v[16];
@@ -46,14 +90,14 @@ SpadTable make_spad(uint64_t seed);
 
 // mode: 0 = tile staged in LDS by DMA (ring for oversize tiles), 1 = per-lane direct, 2 = ring only
 hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
-                           uint64_t* h2, int mode, hipStream_t stream);
+                           uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp = nullptr);
 hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
-                             uint64_t* h2, bool direct, hipStream_t stream);
+                             uint64_t* h2, bool direct, hipStream_t stream, const BucketParams* bp = nullptr);
 
 hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
-                        int variant, hipStream_t stream);
+                        int variant, hipStream_t stream, const BucketParams* bp = nullptr);
 hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
-                      uint64_t* h2, int variant, hipStream_t stream);
+                      uint64_t* h2, int variant, hipStream_t stream, const BucketParams* bp = nullptr);
 hipError_t launch_csr_simple(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                              uint64_t* h2, hipStream_t stream);
 

@@ -68,9 +68,10 @@ __device__ __forceinline__ void st_nt(uint64_t* p, uint64_t v) { __builtin_nonte
 // ---------------------------------------------------------------------------
 // fixed32: key i = keys[32*i .. 32*i+32), keys 16-byte aligned.
 // ---------------------------------------------------------------------------
-template <bool H2, bool ASM, bool NT = false>
+template <bool H2, bool ASM, bool NT = false, bool EPI = false>
 __global__ __launch_bounds__(256) void fnv_fixed32_kernel(const uint4* __restrict__ keys, uint64_t n, uint64_t seed,
-                                                          uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+                                                          uint64_t* __restrict__ h1, uint64_t* __restrict__ h2,
+                                                          BucketParams bp = {}) {
   uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
   uint4 a, b;
@@ -108,6 +109,7 @@ __global__ __launch_bounds__(256) void fnv_fixed32_kernel(const uint4* __restric
     h1[i] = pack(lo, hi);
     if constexpr (H2) h2[i] = pack(lo2, hi2);
   }
+  if constexpr (EPI) bucket_emit(bp, i, pack(lo, hi));
 }
 
 // fixed32, whole key in one asm statement (fnv_key32_x): explicit registers, 64-bit
@@ -125,10 +127,10 @@ __global__ __launch_bounds__(256) void fnv_fixed32_x_kernel(const uint4* __restr
 // fixed: key i = base[L*i .. L*i+L), any L >= 1, any alignment.  The loop trip
 // count is wave-uniform (L is a kernel argument), so no lane diverges.
 // ---------------------------------------------------------------------------
-template <bool H2>
+template <bool H2, bool EPI = false>
 __global__ __launch_bounds__(256) void fnv_fixed_kernel(const uint8_t* __restrict__ base, uint64_t key_len, uint64_t n,
                                                         uint64_t seed, uint64_t* __restrict__ h1,
-                                                        uint64_t* __restrict__ h2) {
+                                                        uint64_t* __restrict__ h2, BucketParams bp = {}) {
   uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
   if (i >= n) return;
   const uint8_t* p = base + key_len * i;
@@ -144,6 +146,14 @@ __global__ __launch_bounds__(256) void fnv_fixed_kernel(const uint8_t* __restric
   }
   h1[i] = pack(lo, hi);
   if constexpr (H2) h2[i] = pack(lo2, hi2);
+  if constexpr (EPI) bucket_emit(bp, i, pack(lo, hi));
+}
+
+// Standalone bucket-index epilogue over hashes in device memory.
+__global__ __launch_bounds__(256) void bucket_index_kernel(const uint64_t* __restrict__ h1, uint64_t n,
+                                                           BucketParams bp) {
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i < n) bucket_emit(bp, i, __builtin_nontemporal_load(h1 + i));
 }
 
 // ---------------------------------------------------------------------------
@@ -391,12 +401,20 @@ static unsigned ring_grid(int variant, bool h2, uint64_t ntiles) {
   return (unsigned)(ntiles < g ? ntiles : g);
 }
 
+hipError_t launch_bucket_index(const uint64_t* h1, uint64_t n, const BucketParams& bp, hipStream_t stream) {
+  if (n == 0 || !(bp.kindex || bp.ckindex)) return hipSuccess;
+  bucket_index_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n, bp);
+  return hipGetLastError();
+}
+
 hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
-                        int variant, hipStream_t stream) {
+                        int variant, hipStream_t stream, const BucketParams* bp) {
   if (n == 0) return hipSuccess;
+  const bool epi = bp && (bp->kindex || bp->ckindex);
   if (!keys || key_len == 0) {
     fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n);
     if (h2) fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h2, n);
+    if (epi) return launch_bucket_index(h1, n, *bp, stream);
     return hipGetLastError();
   }
   bool aligned16 = ((uintptr_t)keys & 15u) == 0;
@@ -408,6 +426,11 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
         else fnv_fixed32_kernel<false, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
       case kVariantAuto:
+        if (epi) {
+          if (h2) fnv_fixed32_kernel<true, true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2, *bp);
+          else fnv_fixed32_kernel<false, true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr, *bp);
+          return hipGetLastError();
+        }
         if (h2) fnv_fixed32_kernel<true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_kernel<false, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
@@ -457,6 +480,7 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
         break;
       }
     }
+    if (epi) return launch_bucket_index(h1, n, *bp, stream);  // A/B variants: unfused epilogue
     return hipGetLastError();
   }
   // Routing by key length (tools/fixed_sweep.py on MI355X, 512 MiB of keys per launch):
@@ -464,9 +488,15 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
   // loads, from 128 B on the cooperative line ring.
   if (variant == kVariantAuto) variant = key_len <= 32 ? kVariantFixedTail : key_len < 128 ? kVariantDirect : 0;
   if (variant != kVariantFixedTail)
-    return launch_fixed_long(keys, key_len, n, seed, h1, h2, variant == kVariantDirect, stream);
-  if (h2) fnv_fixed_kernel<true><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)keys, key_len, n, seed, h1, h2);
-  else fnv_fixed_kernel<false><<<grid_for(n), 256, 0, stream>>>((const uint8_t*)keys, key_len, n, seed, h1, nullptr);
+    return launch_fixed_long(keys, key_len, n, seed, h1, h2, variant == kVariantDirect, stream, epi ? bp : nullptr);
+  const uint8_t* kb = (const uint8_t*)keys;
+  if (epi) {
+    if (h2) fnv_fixed_kernel<true, true><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, h2, *bp);
+    else fnv_fixed_kernel<false, true><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, nullptr, *bp);
+  } else {
+    if (h2) fnv_fixed_kernel<true><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, h2);
+    else fnv_fixed_kernel<false><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, nullptr);
+  }
   return hipGetLastError();
 }
 
@@ -519,9 +549,14 @@ hipError_t launch_csr_simple(const void* bytes, const uint64_t* offsets, uint64_
 }
 
 hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
-                      uint64_t* h2, int variant, hipStream_t stream) {
+                      uint64_t* h2, int variant, hipStream_t stream, const BucketParams* bp) {
   if (n == 0) return hipSuccess;
-  if (variant == kVariantSimpleCsr || !bytes) return launch_csr_simple(bytes, offsets, n, seed, h1, h2, stream);
+  const bool epi = bp && (bp->kindex || bp->ckindex);
+  if (variant == kVariantSimpleCsr || !bytes) {
+    hipError_t e = launch_csr_simple(bytes, offsets, n, seed, h1, h2, stream);
+    if (e == hipSuccess && epi) e = launch_bucket_index(h1, n, *bp, stream);
+    return e;
+  }
   return launch_csr_tile(bytes, offsets, n, seed, h1, h2,
                          variant == kVariantDirect      ? 1
                          : variant == kVariantCsrRing   ? 2
@@ -533,7 +568,7 @@ hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, ui
                          : variant == kVariantCsrLean512x4 ? 8
                          : variant == kVariantCsrAlignProbe ? 9
                                                         : 0,
-                         stream);
+                         stream, epi ? bp : nullptr);
 }
 
 }  // namespace k2h

@@ -134,3 +134,49 @@ void oracle_digest(const uint64_t* h, size_t n, uint64_t first_index, uint64_t o
   out[1] = s;
   out[2] = w;
 }
+
+/* ---------------------------------------------------------------------------
+ * Bucket index: the stateless part of K2HShm::GetKIndexPos and
+ * the collision slot of K2HShm::GetCKIndex, restated loop for loop.  The reference
+ * functions are K2HShm members needing the mapped table and libfullock, so they are
+ * not compiled here; this restatement is the checker.
+ * ------------------------------------------------------------------------- */
+/* lib/k2hshm.cc:78-83 K2HShm::MakeMask */
+uint64_t oracle_make_mask(int bitcnt) {
+  uint64_t mask;
+  for (mask = 0UL; 0 < bitcnt; mask = ((mask << 1) | 1UL), bitcnt--);
+  return mask;
+}
+
+/* lib/k2hshm.cc:85-90 K2HShm::GetMaskBitCount */
+int oracle_mask_bitcount(uint64_t mask) {
+  int bitcnt;
+  for (bitcnt = 0; 0 != mask; bitcnt++, mask = (mask >> 1));
+  return bitcnt;
+}
+
+/* lib/k2hshm.cc:810-833 K2HShm::GetKIndexPos (cur_mask = *pCurMask or pHead->cur_mask)
+ * and lib/k2hshm.cc:1093 (hash & collision_mask).  The reference shifts by
+ * GetMaskBitCount(collision_mask), which is 64 for a full mask: x86-64 takes shift
+ * counts mod 64, so `& 63` here states what the reference build computes. */
+void oracle_kindex_pos(uint64_t hash, uint64_t cur_mask, uint64_t collision_mask, uint64_t* kiptr_pos,
+                       uint64_t* kiarray_pos, uint64_t* ckindex) {
+  uint64_t shifted_hash = hash >> (oracle_mask_bitcount(collision_mask) & 63);
+  uint64_t bitmask, tmphash, pos;
+  for (tmphash = shifted_hash & cur_mask, pos = 0UL, bitmask = 0UL; 0 != (tmphash & ~bitmask);
+       pos++, bitmask = ((bitmask << 1) | 1UL));
+  *kiptr_pos = pos;
+  *kiarray_pos = shifted_hash & oracle_make_mask(0 < pos ? (int)(pos - 1) : 0);
+  *ckindex = hash & collision_mask;
+}
+
+/* Batch form with the ABI's packing: kindex = KIPtrArrayPos << 58 | KIArrayPos. */
+void oracle_bucket_index(const uint64_t* h, size_t n, uint64_t cur_mask, uint64_t collision_mask,
+                         uint64_t* kindex, uint64_t* ckindex) {
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t p, a, c;
+    oracle_kindex_pos(h[i], cur_mask, collision_mask, &p, &a, &c);
+    if (kindex) kindex[i] = (p << 58) | a;
+    if (ckindex) ckindex[i] = c;
+  }
+}

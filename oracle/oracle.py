@@ -66,6 +66,12 @@ def lib() -> ctypes.CDLL:
         L.oracle_digest.restype = None
         L.oracle_digest.argtypes = [_p, _sz, _u64, _p]
         L.oracle_splitmix_word.restype, L.oracle_splitmix_word.argtypes = _u64, [_u64, _u64]
+        L.oracle_make_mask.restype, L.oracle_make_mask.argtypes = _u64, [ctypes.c_int]
+        L.oracle_mask_bitcount.restype, L.oracle_mask_bitcount.argtypes = ctypes.c_int, [_u64]
+        L.oracle_kindex_pos.restype = None
+        L.oracle_kindex_pos.argtypes = [_u64, _u64, _u64, _p, _p, _p]
+        L.oracle_bucket_index.restype = None
+        L.oracle_bucket_index.argtypes = [_p, _sz, _u64, _u64, _p, _p]
         _lib = L
     return _lib
 
@@ -163,3 +169,18 @@ def cpubench():
     L.cpu_bench_k2hbench.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(_u64)]
     return L
+
+
+def kindex_pos(h: int, cur_mask: int, collision_mask: int) -> tuple[int, int, int]:
+    """(KIPtrArrayPos, KIArrayPos, ckindex) of one hash (lib/k2hshm.cc:810-833, 1093)."""
+    p, a, c = _u64(), _u64(), _u64()
+    lib().oracle_kindex_pos(h, cur_mask, collision_mask, ctypes.byref(p), ctypes.byref(a), ctypes.byref(c))
+    return p.value, a.value, c.value
+
+
+def bucket_index(h: np.ndarray, cur_mask: int, collision_mask: int):
+    h = np.ascontiguousarray(h).view(np.uint64)
+    k = np.empty(h.size, np.uint64)
+    c = np.empty(h.size, np.uint64)
+    lib().oracle_bucket_index(_ptr(h), h.size, cur_mask, collision_mask, _ptr(k), _ptr(c))
+    return k, c

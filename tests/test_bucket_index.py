@@ -1,0 +1,152 @@
+"""Bucket-index epilogue: K2HShm::GetKIndexPos's stateless part
+(lib/k2hshm.cc:810-833, MakeMask / GetMaskBitCount :78-90) and the collision slot
+(lib/k2hshm.cc:1093), standalone and fused into the hash kernels.
+
+Parity: the HIP epilogue is compared bit-for-bit with the oracle's loop-for-loop
+restatement.  The reference functions are K2HShm members that need the mapped table and
+libfullock, so they cannot be compiled here; the restatement is pinned by the reference's
+own fixture tests/test_linetool_dsave.cmd (k2hlinetool -mask 2 -cmask 2) with its log
+tests/test_linetool.log:2756-2768: key1\\0 and key27\\0 land in one CKINDEX, and `dsave 3`
+(GetElementsByHash from start hash 3, lib/k2hshmdirect.cc:280-323) reaches it.
+"""
+import numpy as np
+import pytest
+
+import k2hash_amd
+from k2hash_amd import batch
+
+MASKS = [(0x3, 0x3), (0xFF, 0xF), (0x0, 0x0), (0x1, 0x0), ((1 << 28) - 1, 0xF), ((1 << 20) - 1, (1 << 12) - 1),
+         ((1 << 58) - 1, 0x0), (0xFF, (1 << 63) | 0xF), (0x7, 0xFFFFFFFFFFFFFFFF)]
+
+
+def _keys_h(oracle, keys):
+    return [oracle.k2h_hash(k) for k in keys]
+
+
+# ------------------------------------------------------------------------- CPU
+def test_mask_helpers_match_reference_loops(oracle):
+    for b in range(0, 65):
+        m = oracle.lib().oracle_make_mask(b)
+        assert m == ((1 << b) - 1 if b < 64 else (1 << 64) - 1)
+        assert oracle.lib().oracle_mask_bitcount(m) == b
+
+
+def test_known_positions(oracle):
+    # 0x0b2bb3288cdb4d49 = k2h_hash("KEY-0000000000000000\0"); default masks 0xFF / 0xF
+    assert oracle.kindex_pos(0x0B2BB3288CDB4D49, 0xFF, 0xF) == (8, 0x54, 0x9)
+    assert oracle.kindex_pos(0, 0xFF, 0xF) == (0, 0, 0)
+    assert oracle.kindex_pos(1 << 4, 0xFF, 0xF) == (1, 0, 0)
+    assert oracle.kindex_pos(0x30, 0xFF, 0xF) == (2, 1, 0)
+
+
+def test_linetool_dsave_fixture_pin(oracle):
+    """tests/test_linetool_dsave.cmd runs k2hlinetool with -mask 2 -cmask 2 (cur_mask 0x3,
+    collision_mask 0x3) and its log shows key1 and key27 saved together by `dsave 3` and
+    restored together (tests/test_linetool.log:2756-2768)."""
+    cur, cm = 0x3, 0x3
+    b1 = oracle.kindex_pos(oracle.k2h_hash(b"key1\0"), cur, cm)
+    b27 = oracle.kindex_pos(oracle.k2h_hash(b"key27\0"), cur, cm)
+    assert b1 == b27  # one CKINDEX holds both elements
+    # GetElementsByHash walks test_hash from 3 to cur_max_hash = (cur << bitcount(cm)) | cm
+    cur_max = (cur << 2) | cm
+    reach = [t for t in range(0, cur_max + 1) if oracle.kindex_pos(t, cur, cm) == b1]
+    assert reach and min(reach) >= 3
+
+
+def test_kindex_packing_helpers():
+    kv = np.array([(8 << 58) | 0x54, 0, (58 << 58) | ((1 << 58) - 1)], np.uint64)
+    pos, arr = batch.unpack_kindex(kv)
+    assert list(pos) == [8, 0, 58]
+    assert list(arr) == [0x54, 0, (1 << 58) - 1]
+
+
+# ------------------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("cur,cm", MASKS)
+def test_standalone_vs_oracle(cuda, oracle, cur, cm):
+    import torch
+    rng = np.random.default_rng(cur ^ (cm & 0xFFFF))
+    h = rng.integers(0, 2**63, 100003, dtype=np.int64).view(np.uint64) * np.uint64(3)
+    h[:8] = [0, 1, 2, 3, 0xFFFFFFFFFFFFFFFF, 1 << 63, 0x0B2BB3288CDB4D49, 16]
+    d = torch.from_numpy(h.view(np.int64).copy()).to(cuda)
+    k, c = k2hash_amd.bucket_index(d, cur, cm)
+    torch.cuda.synchronize()
+    rk, rc = oracle.bucket_index(h, cur, cm)
+    assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
+    assert np.array_equal(c.cpu().numpy().view(np.uint64), rc)
+
+
+@pytest.mark.gpu
+def test_standalone_optional_outputs_and_errors(cuda):
+    import torch
+    d = torch.arange(1000, dtype=torch.int64, device=cuda)
+    k, c = k2hash_amd.bucket_index(d, 0xFF, 0xF, kindex=False)
+    assert k is None and c is not None
+    k, c = k2hash_amd.bucket_index(d, 0xFF, 0xF, ckindex=False)
+    assert c is None and k is not None
+    torch.cuda.synchronize()
+    with pytest.raises(RuntimeError):
+        k2hash_amd.bucket_index(d, (1 << 59) - 1, 0xF)  # cur_mask does not fit the packing
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 4, 12, 16])
+@pytest.mark.parametrize("key_len", [32, 21, 4096, 100])
+def test_fused_fixed_vs_oracle(cuda, oracle, key_len, variant):
+    import torch
+    if key_len != 32 and variant != 0:
+        pytest.skip("A/B variants only differ for 32-byte keys")
+    batch.set_variant(variant)
+    try:
+        n = 70001 if key_len < 1000 else 3001
+        data = oracle.gen_bytes(key_len * n, byte_off=99)
+        r1, r2 = oracle.hash_fixed(data, key_len)
+        keys = torch.from_numpy(data).to(cuda)
+        for cur, cm in [(0xFF, 0xF), ((1 << 28) - 1, 0xF), (0x3, 0x3)]:
+            h1, h2, k, c = k2hash_amd.hash_fixed_index(keys, key_len, cur, cm, second=True)
+            torch.cuda.synchronize()
+            rk, rc = oracle.bucket_index(r1, cur, cm)
+            assert np.array_equal(h1.cpu().numpy().view(np.uint64), r1)
+            assert np.array_equal(h2.cpu().numpy().view(np.uint64), r2)
+            assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
+            assert np.array_equal(c.cpu().numpy().view(np.uint64), rc)
+    finally:
+        batch.set_variant(0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 3, 11, 19])
+def test_fused_csr_vs_oracle(cuda, oracle, variant):
+    import torch
+    batch.set_variant(variant)
+    try:
+        rng = np.random.default_rng(11)
+        L = rng.integers(0, 300, 20000)
+        L[::17] = 0
+        off = np.zeros(L.size + 1, np.int64)
+        off[1:] = np.cumsum(L)
+        data = oracle.gen_bytes(int(off[-1]) + 3)
+        r1, _ = oracle.hash_csr(data, off.astype(np.uint64))
+        h1, h2, k, c = k2hash_amd.hash_csr_index(torch.from_numpy(data).to(cuda), torch.from_numpy(off).to(cuda),
+                                                 0xFFFF, 0xF, ckindex=False)
+        torch.cuda.synchronize()
+        rk, _ = oracle.bucket_index(r1, 0xFFFF, 0xF)
+        assert h2 is None and c is None
+        assert np.array_equal(h1.cpu().numpy().view(np.uint64), r1)
+        assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
+    finally:
+        batch.set_variant(0)
+
+
+@pytest.mark.gpu
+def test_fused_full_size_matches_standalone(cuda, oracle, digests):
+    """Config 2 at full size: the fused epilogue equals the standalone one over the
+    kernel's own h1, whose digest is the reference's."""
+    import torch
+    cfg = digests["fixed32_16M"]
+    keys = batch.synth_bytes(cfg["n"] * 32, cuda)
+    h1, _, k, c = k2hash_amd.hash_fixed_index(keys, 32, 0xFF, 0xF)
+    k2, c2 = k2hash_amd.bucket_index(h1, 0xFF, 0xF)
+    torch.cuda.synchronize()
+    assert [f"{x:016x}" for x in oracle.digest(h1.cpu().numpy().view(np.uint64))] == cfg["h1"]
+    assert torch.equal(k, k2) and torch.equal(c, c2)
