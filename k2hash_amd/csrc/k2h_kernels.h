@@ -36,6 +36,11 @@ enum {
   kVariantCsrLean512x8 = 20,   // csr: 512-key tiles, 8 waves (one group each), 72 KiB stage
   kVariantCsrLean512x4 = 21,   // csr: 512-key tiles, 4 waves, 72 KiB stage (the default kernel without the ring)
   kVariantCsrAlignProbe = 22,  // csr timing probe (WRONG hashes): lean256 with 16-aligned LDS chunk reads
+  kVariantFixed32Blk64 = 23,   // fixed32 flat kernel with 64 / 128 / 512 / 1024-thread blocks
+  kVariantFixed32Blk128 = 24,
+  kVariantFixed32Blk512 = 25,
+  kVariantFixed32Blk1024 = 26,
+  kVariantFixed32Nt256 = 27,   // fixed32: the round-1 default (nt loads/stores, 256-thread blocks)
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with

@@ -68,11 +68,11 @@ __device__ __forceinline__ void st_nt(uint64_t* p, uint64_t v) { __builtin_nonte
 // ---------------------------------------------------------------------------
 // fixed32: key i = keys[32*i .. 32*i+32), keys 16-byte aligned.
 // ---------------------------------------------------------------------------
-template <bool H2, bool ASM, bool NT = false, bool EPI = false>
-__global__ __launch_bounds__(256) void fnv_fixed32_kernel(const uint4* __restrict__ keys, uint64_t n, uint64_t seed,
-                                                          uint64_t* __restrict__ h1, uint64_t* __restrict__ h2,
-                                                          BucketParams bp = {}) {
-  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+template <bool H2, bool ASM, bool NT = false, bool EPI = false, int BS = 256>
+__global__ __launch_bounds__(BS) void fnv_fixed32_kernel(const uint4* __restrict__ keys, uint64_t n, uint64_t seed,
+                                                         uint64_t* __restrict__ h1, uint64_t* __restrict__ h2,
+                                                         BucketParams bp = {}) {
+  uint64_t i = (uint64_t)blockIdx.x * BS + threadIdx.x;
   if (i >= n) return;
   uint4 a, b;
   if constexpr (NT) {
@@ -425,15 +425,41 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
         if (h2) fnv_fixed32_kernel<true, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_kernel<false, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
-      case kVariantAuto:
+      case kVariantAuto: {
+        // one-wave blocks: a finished wave's slot is refilled at once instead of when the
+        // slowest of its block's four waves ends (3-4 % over 256-thread blocks, A/B in
+        // tools/variants.py, variants 0/23/24 of round 1)
+        unsigned g64 = (unsigned)((n + 63) / 64);
         if (epi) {
-          if (h2) fnv_fixed32_kernel<true, true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2, *bp);
-          else fnv_fixed32_kernel<false, true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr, *bp);
+          if (h2) fnv_fixed32_kernel<true, true, true, true, 64><<<g64, 64, 0, stream>>>(k, n, seed, h1, h2, *bp);
+          else fnv_fixed32_kernel<false, true, true, true, 64><<<g64, 64, 0, stream>>>(k, n, seed, h1, nullptr, *bp);
           return hipGetLastError();
         }
+        if (h2) fnv_fixed32_kernel<true, true, true, false, 64><<<g64, 64, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_kernel<false, true, true, false, 64><<<g64, 64, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
+      case kVariantFixed32Nt256:
         if (h2) fnv_fixed32_kernel<true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_kernel<false, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
+      case kVariantFixed32Blk64:
+      case kVariantFixed32Blk128:
+      case kVariantFixed32Blk512:
+      case kVariantFixed32Blk1024: {
+#define K2H_BLK(BSZ)                                                                                          \
+  {                                                                                                          \
+    unsigned gb = (unsigned)((n + BSZ - 1) / BSZ);                                                           \
+    if (h2) fnv_fixed32_kernel<true, true, true, false, BSZ><<<gb, BSZ, 0, stream>>>(k, n, seed, h1, h2);     \
+    else fnv_fixed32_kernel<false, true, true, false, BSZ><<<gb, BSZ, 0, stream>>>(k, n, seed, h1, nullptr); \
+  }
+        if (variant == kVariantFixed32Blk64) K2H_BLK(64)
+        else if (variant == kVariantFixed32Blk128) K2H_BLK(128)
+        else if (variant == kVariantFixed32Blk512) K2H_BLK(512)
+        else K2H_BLK(1024)
+#undef K2H_BLK
+        break;
+      }
       case kVariantFixed32Asm:
         if (h2) fnv_fixed32_x_kernel<true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_x_kernel<false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
