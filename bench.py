@@ -34,6 +34,9 @@ CONFIGS = {
     "fixed32": ("fixed", 1 << 24, 32, "16M x 32B fixed-length keys (BASELINE config 2)"),
     "csr": ("csr", 1 << 26, (8, 256), "64M mixed 8-256B keys, offsets+bytes CSR (BASELINE config 3)"),
     "fixed4096": ("fixed", 1 << 20, 4096, "1M x 4KiB keys (BASELINE config 5)"),
+    # RALLEDATA blobs (hash + subhash + key + value) for a bulk direct set
+    "ralledata": ("ralledata", 1 << 23, ((8, 64), (0, 256)),
+                  "8M records (keys 8-64B, values 0-256B) -> RALLEDATA blobs with precomputed hashes"),
 }
 
 
@@ -125,6 +128,18 @@ def main():
             keys = batch.synth_bytes(n * shape, dev, byte_off=first * shape)
             sets.append((keys, None))
             algo_bytes = n * shape + 8 * n
+        elif kind == "ralledata":
+            (klo, khi), (vlo, vhi) = shape
+            ko = batch.synth_offsets(n, dev, klo, khi, first_key=first)
+            vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7, first_key=first)
+            kb, vb = int(ko[-1].item()), int(vo[-1].item())
+            kd = batch.synth_bytes(kb, dev, byte_off=s * (1 << 36) + rank * (1 << 34))
+            vd = batch.synth_bytes(vb, dev, byte_off=s * (1 << 36) + rank * (1 << 34) + (1 << 33))
+            blob = torch.empty(80 * n + kb + vb, dtype=torch.uint8, device=dev)
+            boff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            sets.append(((kd, ko, vd, vo), (blob, boff)))
+            # minimal traffic: key + value bytes and their offsets in, blobs + blob offsets out
+            algo_bytes = max(algo_bytes, (kb + vb + 16 * (n + 1)) + (80 * n + kb + vb + 8 * (n + 1)))
         else:
             off = batch.synth_offsets(n, dev, shape[0], shape[1], first_key=first)
             data = batch.synth_bytes(int(off[-1].item()), dev, byte_off=s * (1 << 36) + rank * (1 << 34))
@@ -144,6 +159,11 @@ def main():
 
     def step(i):
         keys, off = sets[i & 1]
+        if kind == "ralledata":
+            from k2hash_amd import ralledata
+            (kd, ko, vd, vo), (blob, boff) = keys, off
+            ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff)
+            return
         if args.index:
             import ctypes
             h1, h2 = outs[i & 1]
@@ -222,13 +242,15 @@ def main():
         prof = ROOT / "profiles" / f"traffic_{args.config}{'_index' if args.index else ''}{'_h2' if args.second else ''}.json"
         if prof.exists():
             traffic = json.loads(prof.read_text()).get("hbm_bytes_per_launch")
-        key_bytes = n * (shape if kind == "fixed" else (shape[0] + shape[1]) / 2)
+        key_bytes = n * (shape if kind == "fixed" else (shape[0][0] + shape[0][1]) / 2 if kind == "ralledata"
+                         else (shape[0] + shape[1]) / 2)
         line = {
             "metric": "key hashes/sec + GiB/s (device-resident), batched 32B keys, 1 MI355X"
             if args.config == "fixed32" and not (args.index or args.second)
+            else f"RALLEDATA records/sec (device-resident), {desc}" if kind == "ralledata"
             else f"key hashes{' + bucket indices' if args.index else ''}/sec (device-resident), {desc}",
             "value": value,
-            "unit": "key hashes/s",
+            "unit": "records/s" if kind == "ralledata" else "key hashes/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,

@@ -126,6 +126,36 @@ int k2h_amd_hash_csr_index(const void* bytes, const uint64_t* offsets, uint64_t 
                            uint32_t flags, uint64_t cur_mask, uint64_t collision_mask, uint64_t* kindex,
                            uint64_t* ckindex, void* stream);
 
+/* ---------------------------------------------------------------------------
+ * 4. RALLEDATA producer (bulk direct-set input with precomputed hashes).
+ *
+ * k2h_set_element_by_binary (lib/k2hash.cc:1562-1581) -> K2HShm::SetElementByBinArray
+ * (lib/k2hshmdirect.cc:343-478) inserts an element from a packed RALLEDATA blob
+ * (lib/k2hshmdirect.h:36-47) and TRUSTS its hash / subhash fields: a bulk loader that
+ * builds blobs here never runs the scalar hash per key.  Blob i (layout of
+ * K2HShm::GetElementToBinary, lib/k2hshmdirect.cc:59-88):
+ *   u64 hash = k2h_hash(key), subhash = k2h_second_hash(key),
+ *   u64 key_length, val_length, skey_length, attrs_length,
+ *   u64 key_pos = 80, val_pos, skey_pos, attrs_pos   (offsets from the blob top)
+ *   then key | value | subkeys | attrs bytes.
+ * Records are four CSR streams (bytes + n+1 offsets, offsets relative to the bytes
+ * pointer); a NULL offsets array means that segment is empty for every record.  Blobs
+ * are packed back to back in `out` (k2h_amd_ralledata_size bytes): blob i starts at
+ * 80*i + the bytes of all earlier records, written to blob_off[i] (n+1 entries,
+ * optional).  A K2HBIN for blob i is {out + blob_off[i], blob_off[i+1] - blob_off[i]}.
+ * ------------------------------------------------------------------------- */
+#define K2H_AMD_RALLEDATA_HEADER 80 /* sizeof(RALLEDATA), packed */
+
+uint64_t k2h_amd_ralledata_size(uint64_t n, uint64_t key_bytes, uint64_t val_bytes, uint64_t skey_bytes,
+                                uint64_t attr_bytes);
+int k2h_amd_build_ralledata(const void* keys, const uint64_t* key_off, const void* vals, const uint64_t* val_off,
+                            const void* skeys, const uint64_t* skey_off, const void* attrs, const uint64_t* attr_off,
+                            uint64_t n, void* out, uint64_t* blob_off, uint32_t flags, void* stream);
+int k2h_amd_build_ralledata_host(const void* keys, const uint64_t* key_off, const void* vals,
+                                 const uint64_t* val_off, const void* skeys, const uint64_t* skey_off,
+                                 const void* attrs, const uint64_t* attr_off, uint64_t n, void* out,
+                                 uint64_t* blob_off, uint32_t flags, int device);
+
 /* Identity / diagnostics. */
 const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */
 const char* k2h_amd_strerror(int code); /* message for `code`, with the last HIP error if any */

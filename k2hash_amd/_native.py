@@ -36,6 +36,10 @@ SIGNATURES = {
     "k2h_amd_bucket_index": (ctypes.c_int, [_p, _u64, _u64, _u64, _p, _p, _p]),
     "k2h_amd_hash_fixed_index": (ctypes.c_int, [_p, _u64, _u64, _p, _p, ctypes.c_uint32, _u64, _u64, _p, _p, _p]),
     "k2h_amd_hash_csr_index": (ctypes.c_int, [_p, _p, _u64, _p, _p, ctypes.c_uint32, _u64, _u64, _p, _p, _p]),
+    "k2h_amd_ralledata_size": (_u64, [_u64, _u64, _u64, _u64, _u64]),
+    "k2h_amd_build_ralledata": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _u64, _p, _p, ctypes.c_uint32, _p]),
+    "k2h_amd_build_ralledata_host": (ctypes.c_int,
+                                     [_p, _p, _p, _p, _p, _p, _p, _p, _u64, _p, _p, ctypes.c_uint32, ctypes.c_int]),
     "k2h_amd_version": (ctypes.c_char_p, []),
     "k2h_amd_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "k2h_amd_set_variant": (ctypes.c_int, [ctypes.c_int]),

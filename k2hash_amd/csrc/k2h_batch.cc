@@ -406,6 +406,97 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* byt
   return K2H_AMD_OK;
 }
 
+// ---------------------------------------------------------------------------
+// RALLEDATA producer (include/k2hash_amd.h section 4)
+// ---------------------------------------------------------------------------
+__attribute__((visibility("default"))) uint64_t k2h_amd_ralledata_size(uint64_t n, uint64_t key_bytes,
+                                                                       uint64_t val_bytes, uint64_t skey_bytes,
+                                                                       uint64_t attr_bytes) {
+  return 80ull * n + key_bytes + val_bytes + skey_bytes + attr_bytes;
+}
+
+__attribute__((visibility("default"))) int k2h_amd_build_ralledata(
+    const void* keys, const uint64_t* key_off, const void* vals, const uint64_t* val_off, const void* skeys,
+    const uint64_t* skey_off, const void* attrs, const uint64_t* attr_off, uint64_t n, void* out, uint64_t* blob_off,
+    uint32_t flags, void* stream) {
+  if (!key_off) return fail(K2H_AMD_EINVAL, "key_off is NULL");
+  if (n && !out) return fail(K2H_AMD_EINVAL, "out is NULL");
+  if ((val_off && !vals) || (skey_off && !skeys) || (attr_off && !attrs))
+    return fail(K2H_AMD_EINVAL, "segment offsets without segment bytes");
+  k2h::RalleInputs in;
+  in.keys = (const uint8_t*)keys;
+  in.koff = key_off;
+  in.vals = (const uint8_t*)vals;
+  in.voff = val_off;
+  in.skeys = (const uint8_t*)skeys;
+  in.soff = skey_off;
+  in.attrs = (const uint8_t*)attrs;
+  in.aoff = attr_off;
+  hipError_t e = k2h::launch_ralledata(in, n, seed_for(flags), (uint8_t*)out, blob_off, variant(), (hipStream_t)stream);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_ralledata", e);
+}
+
+// Host form: stage each segment's byte range and offsets on `device`, build there, copy
+// the blobs (and offsets) back.  One shot, not pipelined.
+__attribute__((visibility("default"))) int k2h_amd_build_ralledata_host(
+    const void* keys, const uint64_t* key_off, const void* vals, const uint64_t* val_off, const void* skeys,
+    const uint64_t* skey_off, const void* attrs, const uint64_t* attr_off, uint64_t n, void* out, uint64_t* blob_off,
+    uint32_t flags, int device) {
+  if (!key_off) return fail(K2H_AMD_EINVAL, "key_off is NULL");
+  if (n == 0) {
+    if (blob_off) blob_off[0] = 0;
+    return K2H_AMD_OK;
+  }
+  if (!out) return fail(K2H_AMD_EINVAL, "out is NULL");
+  const void* src[4] = {keys, vals, skeys, attrs};
+  const uint64_t* off[4] = {key_off, val_off, skey_off, attr_off};
+  uint64_t total = 80ull * n;
+  for (int s = 0; s < 4; ++s) {
+    if (!off[s]) continue;
+    if (!src[s] && off[s][n] != off[s][0]) return fail(K2H_AMD_EINVAL, "segment offsets without segment bytes");
+    for (uint64_t i = 0; i < n; ++i)
+      if (off[s][i + 1] < off[s][i]) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
+    total += off[s][n] - off[s][0];
+  }
+  int rc = set_device(device);
+  if (rc) return rc;
+  hipStream_t st;
+  hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+  if (e != hipSuccess) return fail(K2H_AMD_EHIP, "hipStreamCreate", e);
+  void* dbuf[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint64_t* doff[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint8_t* dout = nullptr;
+  uint64_t* dblob = nullptr;
+  k2h::RalleInputs in;
+  const uint8_t** bp[4] = {&in.keys, &in.vals, &in.skeys, &in.attrs};
+  const uint64_t** op[4] = {&in.koff, &in.voff, &in.soff, &in.aoff};
+  for (int s = 0; s < 4 && e == hipSuccess; ++s) {
+    if (!off[s]) continue;
+    uint64_t lo = off[s][0], len = off[s][n] - lo;
+    e = hipMallocAsync((void**)&doff[s], (n + 1) * 8, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(doff[s], off[s], (n + 1) * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipMallocAsync(&dbuf[s], len ? len : 1, st);
+    if (e == hipSuccess && len) e = hipMemcpyAsync(dbuf[s], (const uint8_t*)src[s] + lo, len, hipMemcpyHostToDevice, st);
+    *bp[s] = (const uint8_t*)dbuf[s] - lo;  // kernel indexes with the caller's raw offsets
+    *op[s] = doff[s];
+  }
+  if (e == hipSuccess) e = hipMallocAsync((void**)&dout, total, st);
+  if (e == hipSuccess && blob_off) e = hipMallocAsync((void**)&dblob, (n + 1) * 8, st);
+  if (e == hipSuccess) e = k2h::launch_ralledata(in, n, seed_for(flags), dout, dblob, variant(), st);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess && blob_off) e = hipMemcpyAsync(blob_off, dblob, (n + 1) * 8, hipMemcpyDeviceToHost, st);
+  for (int s = 0; s < 4; ++s) {
+    if (dbuf[s]) (void)hipFreeAsync(dbuf[s], st);
+    if (doff[s]) (void)hipFreeAsync(doff[s], st);
+  }
+  if (dout) (void)hipFreeAsync(dout, st);
+  if (dblob) (void)hipFreeAsync(dblob, st);
+  hipError_t f = hipStreamSynchronize(st);
+  (void)hipStreamDestroy(st);
+  if (e == hipSuccess) e = f;
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "build_ralledata_host", e);
+}
+
 __attribute__((visibility("default"))) const char* k2h_amd_version(void) {
   return "k2hash_amd 0.1 (FNV-1A BUILTIN, gfx950 HIP batch kernels)";
 }

@@ -41,6 +41,7 @@ enum {
   kVariantFixed32Blk512 = 25,
   kVariantFixed32Blk1024 = 26,
   kVariantFixed32Nt256 = 27,   // fixed32: the round-1 default (nt loads/stores, 256-thread blocks)
+  kVariantRalleThread = 28,    // ralledata: one thread per record (default: 16 lanes per record)
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with
@@ -86,6 +87,21 @@ __device__ __forceinline__ void bucket_emit(const BucketParams& bp, uint64_t i, 
 
 // Standalone epilogue over hashes already in device memory.
 hipError_t launch_bucket_index(const uint64_t* h1, uint64_t n, const BucketParams& bp, hipStream_t stream);
+
+// RALLEDATA producer inputs (k2h_ralledata.hip): four CSR streams; a null offsets
+// array = that segment is empty for every record.
+struct RalleInputs {
+  const uint8_t* keys = nullptr;
+  const uint64_t* koff = nullptr;
+  const uint8_t* vals = nullptr;
+  const uint64_t* voff = nullptr;
+  const uint8_t* skeys = nullptr;
+  const uint64_t* soff = nullptr;
+  const uint8_t* attrs = nullptr;
+  const uint64_t* aoff = nullptr;
+};
+hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, uint8_t* out, uint64_t* blob_off,
+                            int variant, hipStream_t stream);
 
 // S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).
 struct SpadTable {

@@ -1,0 +1,142 @@
+// k2hash_amd -- RALLEDATA producer.
+//
+// k2hash's direct-set path takes elements as packed RALLEDATA blobs that already carry
+// the key's hash and subhash (struct at lib/k2hshmdirect.h:36-47; consumed by
+// K2HShm::SetElementByBinArray, lib/k2hshmdirect.cc:343-478, via
+// k2h_set_element_by_binary, lib/k2hash.cc:1562-1581): a bulk loader that builds the
+// blobs on the GPU never runs the scalar hash per key.  Blob layout = the one
+// K2HShm::GetElementToBinary writes (lib/k2hshmdirect.cc:59-88):
+//   [0]  hash  = k2h_hash(key)          [8]  subhash = k2h_second_hash(key)
+//   [16] key_length  [24] val_length  [32] skey_length  [40] attrs_length
+//   [48] key_pos = 80  [56] val_pos  [64] skey_pos  [72] attrs_pos   (from the blob top)
+//   [80] key | value | subkeys | attrs
+// Records come as four CSR streams (keys, values, subkeys, attributes: bytes + n+1
+// offsets; a NULL offsets array means the segment is empty for every record).  Blobs are
+// packed back to back, so blob i starts at the closed form
+//   80 i + sum over segments of (seg_off[i] - seg_off[0])
+// and no scan is needed.
+//
+// Two kernels: the CSR hash kernel (k2h_csr.hip) writes h1/h2 to a stream-ordered
+// scratch buffer, then an assembly kernel writes the blobs (16 lanes per record by
+// default; one thread per record as the A/B variant).  Blob and segment addresses are
+// byte-aligned; the global path handles the unaligned 16-byte accesses.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "k2h_kernels.h"
+
+namespace k2h {
+namespace {
+
+typedef uint64_t u64_ua __attribute__((aligned(1)));
+typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
+
+__device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len) {
+  uint64_t j = 0;
+  for (; j + 16 <= len; j += 16) *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
+  for (; j < len; ++j) dst[j] = src[j];
+}
+
+__device__ __forceinline__ uint64_t seg_len(const uint64_t* off, uint64_t i) { return off ? off[i + 1] - off[i] : 0; }
+__device__ __forceinline__ uint64_t seg_before(const uint64_t* off, uint64_t i) { return off ? off[i] - off[0] : 0; }
+
+__global__ __launch_bounds__(256) void ralledata_assemble_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
+                                                                 uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
+  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i), al = seg_len(in.aoff, i);
+  const uint64_t o = 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) +
+                     seg_before(in.aoff, i);
+  uint8_t* b = out + o;
+  u64_ua* hd = reinterpret_cast<u64_ua*>(b);
+  hd[0] = h[i];
+  hd[1] = h[n + i];
+  hd[2] = kl;
+  hd[3] = vl;
+  hd[4] = sl;
+  hd[5] = al;
+  hd[6] = 80;
+  hd[7] = 80 + kl;
+  hd[8] = 80 + kl + vl;
+  hd[9] = 80 + kl + vl + sl;
+  if (kl) copy_bytes(b + 80, in.keys + in.koff[i], kl);
+  if (vl) copy_bytes(b + 80 + kl, in.vals + in.voff[i], vl);
+  if (sl) copy_bytes(b + 80 + kl + vl, in.skeys + in.soff[i], sl);
+  if (al) copy_bytes(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al);
+  if (blob_off) {
+    blob_off[i] = o;
+    if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
+  }
+}
+
+// Group form (default): 16 lanes per record, 4 records per wave.  Lane q of a group
+// writes header piece q (5 x 16 B) and copies bytes [16q + 256j, +16) of each segment,
+// so a group's loads and stores are consecutive 16-byte pieces (256 B per instruction
+// per group) instead of one lane streaming a whole record; the last partial piece of a
+// segment is copied one byte per lane.
+constexpr int kGroup = 16;
+
+__device__ __forceinline__ void group_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len,
+                                           uint32_t q) {
+  uint64_t full = len & ~15ull;
+  for (uint64_t j = 16ull * q; j < full; j += 16ull * kGroup)
+    *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
+  uint64_t t = full + q;  // the <= 15 tail bytes: one byte per lane, one instruction
+  if (t < len) dst[t] = src[t];
+}
+
+__global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
+                                                              uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
+  const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / kGroup;
+  const uint32_t q = threadIdx.x % kGroup;
+  if (i >= n) return;
+  const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i), al = seg_len(in.aoff, i);
+  const uint64_t o = 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) +
+                     seg_before(in.aoff, i);
+  uint8_t* b = out + o;
+  if (q < 5) {
+    uint64_t f0, f1;
+    switch (q) {
+      case 0: f0 = h[i]; f1 = h[n + i]; break;
+      case 1: f0 = kl; f1 = vl; break;
+      case 2: f0 = sl; f1 = al; break;
+      case 3: f0 = 80; f1 = 80 + kl; break;
+      default: f0 = 80 + kl + vl; f1 = 80 + kl + vl + sl; break;
+    }
+    *reinterpret_cast<u32x4_ua*>(b + 16 * q) =
+        u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
+  }
+  if (kl) group_copy(b + 80, in.keys + in.koff[i], kl, q);
+  if (vl) group_copy(b + 80 + kl, in.vals + in.voff[i], vl, q);
+  if (sl) group_copy(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
+  if (al) group_copy(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
+  if (blob_off && q == 0) {
+    blob_off[i] = o;
+    if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, uint8_t* out, uint64_t* blob_off,
+                            int variant, hipStream_t stream) {
+  if (n == 0) {
+    if (blob_off) return hipMemsetAsync(blob_off, 0, 8, stream);
+    return hipSuccess;
+  }
+  uint64_t* h = nullptr;
+  hipError_t e = hipMallocAsync((void**)&h, 16 * n, stream);
+  if (e != hipSuccess) return e;
+  e = launch_csr(in.keys, in.koff, n, seed, h, h + n, variant, stream);
+  if (e == hipSuccess) {
+    if (variant == kVariantRalleThread)
+      ralledata_assemble_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else
+      ralledata_group_kernel<<<(unsigned)((n * kGroup + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    e = hipGetLastError();
+  }
+  hipError_t f = hipFreeAsync(h, stream);
+  return e != hipSuccess ? e : f;
+}
+
+}  // namespace k2h

@@ -180,3 +180,49 @@ void oracle_bucket_index(const uint64_t* h, size_t n, uint64_t cur_mask, uint64_
     if (ckindex) ckindex[i] = c;
   }
 }
+
+/* ---------------------------------------------------------------------------
+ * RALLEDATA producer, restated: one packed blob per record,
+ * laid out as K2HShm::GetElementToBinary does (lib/k2hshmdirect.cc:59-88) on the
+ * packed struct of lib/k2hshmdirect.h:36-47 (10 little-endian 8-byte fields:
+ * hash, subhash, key/val/skey/attrs lengths, key/val/skey/attrs positions from the
+ * struct top), hash/subhash = k2h_hash / k2h_second_hash of the key
+ * (lib/k2hshm.cc:2184-2185).  Blobs are packed back to back: blob i starts at
+ * 80*i + sum of the bytes of records < i.  Segment offset arrays may be NULL
+ * (segment empty for every record).  Pinned by tests/golden/ralledata.json, which
+ * oracle/gen_ralledata.cc writes from the reference's own header and hash build.
+ * ------------------------------------------------------------------------- */
+static void put64(uint8_t* p, uint64_t v) {
+  for (int i = 0; i < 8; ++i) p[i] = (uint8_t)(v >> (8 * i));
+}
+
+uint64_t oracle_build_ralledata(const uint8_t* keys, const uint64_t* koff, const uint8_t* vals, const uint64_t* voff,
+                                const uint8_t* skeys, const uint64_t* soff, const uint8_t* attrs,
+                                const uint64_t* aoff, size_t n, uint8_t* out, uint64_t* blob_off, int variant) {
+  uint64_t o = 0;
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t kl = koff[i + 1] - koff[i];
+    uint64_t vl = voff ? voff[i + 1] - voff[i] : 0;
+    uint64_t sl = soff ? soff[i + 1] - soff[i] : 0;
+    uint64_t al = aoff ? aoff[i + 1] - aoff[i] : 0;
+    if (blob_off) blob_off[i] = o;
+    uint8_t* b = out + o;
+    put64(b + 0, oracle_k2h_hash(keys + koff[i], kl, variant));
+    put64(b + 8, oracle_k2h_second_hash(keys + koff[i], kl, variant));
+    put64(b + 16, kl);
+    put64(b + 24, vl);
+    put64(b + 32, sl);
+    put64(b + 40, al);
+    put64(b + 48, 80);
+    put64(b + 56, 80 + kl);
+    put64(b + 64, 80 + kl + vl);
+    put64(b + 72, 80 + kl + vl + sl);
+    if (kl) memcpy(b + 80, keys + koff[i], kl);
+    if (vl) memcpy(b + 80 + kl, vals + voff[i], vl);
+    if (sl) memcpy(b + 80 + kl + vl, skeys + soff[i], sl);
+    if (al) memcpy(b + 80 + kl + vl + sl, attrs + aoff[i], al);
+    o += 80 + kl + vl + sl + al;
+  }
+  if (blob_off) blob_off[n] = o;
+  return o;
+}

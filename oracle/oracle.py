@@ -70,6 +70,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_mask_bitcount.restype, L.oracle_mask_bitcount.argtypes = ctypes.c_int, [_u64]
         L.oracle_kindex_pos.restype = None
         L.oracle_kindex_pos.argtypes = [_u64, _u64, _u64, _p, _p, _p]
+        L.oracle_build_ralledata.restype = _u64
+        L.oracle_build_ralledata.argtypes = [_p, _p, _p, _p, _p, _p, _p, _p, _sz, _p, _p, ctypes.c_int]
         L.oracle_bucket_index.restype = None
         L.oracle_bucket_index.argtypes = [_p, _sz, _u64, _u64, _p, _p]
         _lib = L
@@ -184,3 +186,26 @@ def bucket_index(h: np.ndarray, cur_mask: int, collision_mask: int):
     c = np.empty(h.size, np.uint64)
     lib().oracle_bucket_index(_ptr(h), h.size, cur_mask, collision_mask, _ptr(k), _ptr(c))
     return k, c
+
+
+def _csr_of(parts):
+    data = np.frombuffer(b"".join(parts), np.uint8) if any(parts) else np.zeros(1, np.uint8)
+    off = np.zeros(len(parts) + 1, np.uint64)
+    off[1:] = np.cumsum([len(x) for x in parts])
+    return np.ascontiguousarray(data), off
+
+
+def build_ralledata(keys, vals=None, skeys=None, attrs=None, variant: int = 0):
+    """RALLEDATA blobs for records given as lists of bytes (None = segment empty for all).
+    Returns (blob bytes as uint8 array, blob offsets n+1)."""
+    n = len(keys)
+    segs = [_csr_of(keys)] + [(_csr_of(x) if x is not None else (np.zeros(1, np.uint8), None))
+                             for x in (vals, skeys, attrs)]
+    total = 80 * n + sum(int(o[-1]) for _, o in segs if o is not None)
+    out = np.zeros(max(total, 1), np.uint8)
+    boff = np.zeros(n + 1, np.uint64)
+    args = []
+    for d, o in segs:
+        args += [_ptr(d), _ptr(o) if o is not None else None]
+    lib().oracle_build_ralledata(*args, n, _ptr(out), _ptr(boff), variant)
+    return out[:total], boff

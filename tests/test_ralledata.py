@@ -1,0 +1,138 @@
+"""RALLEDATA producer: GPU-built direct-set blobs vs the
+reference layout.
+
+Pins: tests/golden/ralledata.json is written by oracle/gen_ralledata.cc, which is
+compiled against the REFERENCE's own lib/k2hash.h + lib/k2hshmdirect.h (struct
+RALLEDATA, ralledata_init, calc_ralledata_length) and hashes with the reference's
+lib/k2hashfunc.cc build, laying blobs out as K2HShm::GetElementToBinary does
+(lib/k2hshmdirect.cc:59-88).  The oracle restatement (oracle_build_ralledata) must equal
+it byte for byte; the HIP producer must equal both.
+"""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+from k2hash_amd import ralledata
+
+
+@pytest.fixture(scope="module")
+def golden():
+    g = json.loads((GOLDEN / "ralledata.json").read_text())
+    recs = g["records"]
+    b = bytes.fromhex
+    return g, [b(r["key"]) for r in recs], [b(r["val"]) for r in recs], [b(r["skey"]) for r in recs], \
+        [b(r["attrs"]) for r in recs], b"".join(b(r["blob"]) for r in recs)
+
+
+# ------------------------------------------------------------------------- CPU
+def test_reference_struct_layout(golden):
+    g = golden[0]
+    assert g["sizeof_RALLEDATA"] == ralledata.HEADER == 80
+    assert [g["offsets"][f] for f in ralledata._FIELDS] == list(range(0, 80, 8))
+
+
+def test_oracle_matches_reference_fixture(oracle, golden):
+    _, k, v, s, a, blob = golden
+    out, boff = oracle.build_ralledata(k, v, s, a)
+    assert out.tobytes() == blob
+    assert int(boff[-1]) == len(blob)
+
+
+def test_parse_blob_fields(oracle, golden):
+    _, k, v, s, a, blob = golden
+    o = 0
+    for i in range(len(k)):
+        n = 80 + len(k[i]) + len(v[i]) + len(s[i]) + len(a[i])
+        p = ralledata.parse_blob(blob[o:o + n])
+        assert (p.key, p.val, p.skey, p.attrs) == (k[i], v[i], s[i], a[i])
+        assert p.hash == oracle.k2h_hash(k[i]) and p.subhash == oracle.k2h_second_hash(k[i])
+        o += n
+    assert o == len(blob)
+
+
+def test_empty_batch_needs_no_gpu():
+    out, boff = ralledata.build_ralledata_host([])
+    assert out.size == 0 and list(boff) == [0]
+
+
+# ------------------------------------------------------------------------- GPU
+def _dev(torch, cuda, parts):
+    data = np.frombuffer(b"".join(parts), np.uint8).copy() if any(parts) else np.zeros(1, np.uint8)
+    off = np.zeros(len(parts) + 1, np.int64)
+    off[1:] = np.cumsum([len(x) for x in parts])
+    return torch.from_numpy(data).to(cuda), torch.from_numpy(off).to(cuda)
+
+
+@pytest.mark.gpu
+def test_device_matches_reference_fixture(cuda, golden):
+    import torch
+    _, k, v, s, a, blob = golden
+    segs = [_dev(torch, cuda, x) for x in (k, v, s, a)]
+    out, boff = ralledata.build_ralledata(*segs[0], *segs[1], *segs[2], *segs[3])
+    torch.cuda.synchronize()
+    assert out.cpu().numpy().tobytes() == blob
+    o = boff.cpu().numpy()
+    assert o[0] == 0 and o[-1] == len(blob)
+
+
+@pytest.mark.gpu
+def test_host_matches_reference_fixture(cuda, golden):
+    _, k, v, s, a, blob = golden
+    out, boff = ralledata.build_ralledata_host(k, v, s, a)
+    assert out.tobytes() == blob and int(boff[-1]) == len(blob)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("variant", [0, 28])
+@pytest.mark.parametrize("segments", ["kv", "k", "kvsa", "ka"])
+def test_device_vs_oracle_random(cuda, oracle, segments, variant):
+    import torch
+    from k2hash_amd import batch
+    batch.set_variant(variant)
+    rng = np.random.default_rng(len(segments))
+    n = 50021
+    data = oracle.gen_bytes(n * 700, byte_off=1234)
+    pos = 0
+
+    def take(lo, hi, p_empty):
+        nonlocal pos
+        out = []
+        for _ in range(n):
+            L = 0 if rng.random() < p_empty else int(rng.integers(lo, hi))
+            out.append(data[pos:pos + L].tobytes())
+            pos += L
+        return out
+    k = take(1, 300, 0.0)
+    v = take(0, 260, 0.2) if "v" in segments else None
+    s = take(0, 40, 0.5) if "s" in segments else None
+    a = take(0, 60, 0.5) if "a" in segments else None
+    ref, rboff = oracle.build_ralledata(k, v, s, a)
+    segs = []
+    for x in (k, v, s, a):
+        segs += list(_dev(torch, cuda, x)) if x is not None else [None, None]
+    try:
+        out, boff = ralledata.build_ralledata(*segs)
+        torch.cuda.synchronize()
+    finally:
+        batch.set_variant(0)
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert np.array_equal(boff.cpu().numpy().view(np.uint64), rboff)
+
+
+@pytest.mark.gpu
+def test_device_nonzero_first_offsets(cuda, oracle):
+    """Offsets relative to the byte pointers need not start at 0 (a window of a larger
+    batch), and the blob offsets are relative to the window."""
+    import torch
+    k = [bytes([i % 251]) * (1 + i % 37) for i in range(3000)]
+    v = [bytes([i % 13]) * (i % 50) for i in range(3000)]
+    ref, rboff = oracle.build_ralledata(k[1000:], v[1000:])
+    kd, ko = _dev(torch, cuda, k)
+    vd, vo = _dev(torch, cuda, v)
+    out, boff = ralledata.build_ralledata(kd, ko[1000:].contiguous(), vd, vo[1000:].contiguous())
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert np.array_equal(boff.cpu().numpy().view(np.uint64), rboff)
