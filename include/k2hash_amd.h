@@ -156,6 +156,45 @@ int k2h_amd_build_ralledata_host(const void* keys, const uint64_t* key_off, cons
                                  const void* attrs, const uint64_t* attr_off, uint64_t n, void* out,
                                  uint64_t* blob_off, uint32_t flags, int device);
 
+/* ---------------------------------------------------------------------------
+ * 5. Bulk key streams: keys anywhere in a buffer, and k2hash archives.
+ *
+ * k2h_amd_hash_ranges hashes key i = base[starts[i], starts[i] + lens[i]) (device
+ * pointers).  With K2H_AMD_FLAG_CSTR each key is hashed as the C string that
+ * K2HShm::Set(const char*, ...) stores (lib/k2hshm.cc:2081-2083): the range plus a
+ * terminating NUL (strlen + 1 bytes) -- the form k2himport's TSV / mdbm loaders use
+ * (tests/k2himport.cc:81-112).  The call synchronises `stream` once (to size the
+ * staging buffer the keys are packed into).
+ *
+ * k2h_amd_archive_scan walks a k2hash archive (K2HArchive::Save / Load,
+ * lib/k2harchive.cc:82-383; record = packed 104-byte SCOM header + data,
+ * lib/k2hcommand.h:64-79) as Load does and reports each record; recs may be NULL to
+ * count only.  k2h_amd_archive_prehash_host then hashes every record's key on the GPU
+ * (and, if new_h1/new_h2 are given, the new key of each SCOM_RENAME record), so a
+ * loader can have all hashes before applying record one.  Host pointers.
+ * ------------------------------------------------------------------------- */
+#define K2H_AMD_FLAG_CSTR 0x2u /* hash each key as key + NUL (K2HShm::Set(const char*)) */
+
+int k2h_amd_hash_ranges(const void* base, const uint64_t* starts, const uint64_t* lens, uint64_t n, uint64_t* h1,
+                        uint64_t* h2, uint32_t flags, void* stream);
+
+#define K2H_AMD_ARCHIVE_BAD_TYPE 1  /* type outside SCOM_TYPE_MIN..MAX (Load: skip / fail) */
+#define K2H_AMD_ARCHIVE_TRUNCATED 2 /* a data segment runs past the end of the file */
+typedef struct k2h_amd_archive_rec {
+  int64_t type;    /* SCOM_SET_ALL .. SCOM_RENAME (lib/k2hcommand.h:47-55) */
+  uint64_t offset; /* record start in the file */
+  uint64_t key_off, key_len, val_off, val_len, skey_off, skey_len, attrs_off, attrs_len, exdata_off, exdata_len;
+  /* absolute offsets in the file */
+  int32_t status;  /* 0, K2H_AMD_ARCHIVE_BAD_TYPE or K2H_AMD_ARCHIVE_TRUNCATED */
+  int32_t reserved;
+} k2h_amd_archive_rec;
+
+int k2h_amd_archive_scan(const void* file, uint64_t size, k2h_amd_archive_rec* recs, uint64_t cap,
+                         uint64_t* count);
+int k2h_amd_archive_prehash_host(const void* file, uint64_t size, const k2h_amd_archive_rec* recs, uint64_t count,
+                                 uint64_t* h1, uint64_t* h2, uint64_t* new_h1, uint64_t* new_h2, uint32_t flags,
+                                 int device);
+
 /* Identity / diagnostics. */
 const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */
 const char* k2h_amd_strerror(int code); /* message for `code`, with the last HIP error if any */

@@ -20,6 +20,7 @@ K2H_AMD_EHIP = -2
 K2H_AMD_ENOMEM = -3
 K2H_AMD_ENODEV = -4
 K2H_AMD_FLAG_STD_FNV = 0x1
+K2H_AMD_FLAG_CSTR = 0x2
 
 _u64 = ctypes.c_uint64
 _p = ctypes.c_void_p
@@ -40,6 +41,9 @@ SIGNATURES = {
     "k2h_amd_build_ralledata": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _u64, _p, _p, ctypes.c_uint32, _p]),
     "k2h_amd_build_ralledata_host": (ctypes.c_int,
                                      [_p, _p, _p, _p, _p, _p, _p, _p, _u64, _p, _p, ctypes.c_uint32, ctypes.c_int]),
+    "k2h_amd_hash_ranges": (ctypes.c_int, [_p, _p, _p, _u64, _p, _p, ctypes.c_uint32, _p]),
+    "k2h_amd_archive_scan": (ctypes.c_int, [_p, _u64, _p, _u64, _p]),
+    "k2h_amd_archive_prehash_host": (ctypes.c_int, [_p, _u64, _p, _u64, _p, _p, _p, _p, ctypes.c_uint32, ctypes.c_int]),
     "k2h_amd_version": (ctypes.c_char_p, []),
     "k2h_amd_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "k2h_amd_set_variant": (ctypes.c_int, [ctypes.c_int]),
@@ -72,6 +76,14 @@ def batch_lib() -> ctypes.CDLL:
     """The batch library (HIP kernels + plugin symbols).  Raises if not built."""
     global _batch
     if _batch is None:
+        # One HIP runtime per process: torch ships its own libamdhip64 (soname
+        # libamdhip64.so.7, like /opt/rocm's).  Loading torch first lets this library's
+        # libamdhip64.so.7 dependency bind to that copy; the other order leaves two
+        # runtimes in the process and torch then sees no GPU.
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not BATCH_LIB.exists():
             raise RuntimeError(
                 f"k2hash_amd native library missing: {BATCH_LIB} "

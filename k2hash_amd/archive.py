@@ -1,0 +1,80 @@
+"""Bulk key streams: keys at arbitrary ranges of a buffer, and
+k2hash archive files (include/k2hash_amd.h section 5).
+
+An archive is what K2HArchive::Save writes and K2HArchive::Load replays record by
+record, hashing each key on the CPU inside ReplaceAll / Remove / Rename
+(lib/k2harchive.cc:82-383).  scan() walks the records the way Load does; prehash()
+hashes every key of the file in one GPU batch.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _native
+from .batch import FLAG_STD_FNV, _check_dev, _dev_ptr, _stream_handle, _torch
+
+FLAG_CSTR = _native.K2H_AMD_FLAG_CSTR
+SCOM_SET_ALL, SCOM_REPLACE_VAL, SCOM_REPLACE_SKEY, SCOM_DEL_KEY, SCOM_OW_VAL, SCOM_REPLACE_ATTRS, SCOM_RENAME = range(7)
+STATUS_OK, STATUS_BAD_TYPE, STATUS_TRUNCATED = 0, 1, 2
+
+# struct k2h_amd_archive_rec (include/k2hash_amd.h)
+REC_DTYPE = np.dtype([("type", "<i8"), ("offset", "<u8"), ("key_off", "<u8"), ("key_len", "<u8"),
+                      ("val_off", "<u8"), ("val_len", "<u8"), ("skey_off", "<u8"), ("skey_len", "<u8"),
+                      ("attrs_off", "<u8"), ("attrs_len", "<u8"), ("exdata_off", "<u8"), ("exdata_len", "<u8"),
+                      ("status", "<i4"), ("reserved", "<i4")])
+
+
+def _buf(data) -> np.ndarray:
+    return np.frombuffer(data, np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) else \
+        np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+
+
+def scan(data) -> np.ndarray:
+    """Records of an archive (structured array, REC_DTYPE), in file order."""
+    f = _buf(data)
+    ptr = ctypes.c_void_p(f.ctypes.data if f.size else 1)
+    lib = _native.batch_lib()
+    cnt = ctypes.c_uint64()
+    _native.check(lib.k2h_amd_archive_scan(ptr, f.size, None, 0, ctypes.byref(cnt)))
+    recs = np.zeros(cnt.value, REC_DTYPE)
+    _native.check(lib.k2h_amd_archive_scan(ptr, f.size, ctypes.c_void_p(recs.ctypes.data if recs.size else 1),
+                                           recs.size, ctypes.byref(cnt)))
+    return recs
+
+
+def prehash(data, recs=None, rename: bool = False, std_fnv: bool = False, device: int = 0):
+    """(h1, h2[, new_h1, new_h2]) of every record's key (uint64 arrays, 0 for records whose
+    status is not STATUS_OK); with rename=True also the new key of SCOM_RENAME records."""
+    f = _buf(data)
+    if recs is None:
+        recs = scan(f)
+    n = recs.size
+    h1, h2 = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    nh1, nh2 = (np.zeros(n, np.uint64), np.zeros(n, np.uint64)) if rename else (None, None)
+    p = lambda a: ctypes.c_void_p(a.ctypes.data) if a is not None else None  # noqa: E731
+    if n:
+        _native.check(_native.batch_lib().k2h_amd_archive_prehash_host(
+            ctypes.c_void_p(f.ctypes.data if f.size else 1), f.size, p(recs), n, p(h1), p(h2), p(nh1), p(nh2),
+            FLAG_STD_FNV if std_fnv else 0, device))
+    return (h1, h2, nh1, nh2) if rename else (h1, h2)
+
+
+def hash_ranges(base, starts, lens, second: bool = False, cstr: bool = False, std_fnv: bool = False, stream=None):
+    """Device form: key i = base[starts[i] : starts[i] + lens[i]] (uint8 / int64 / int64
+    device tensors).  cstr=True hashes key + NUL (K2HShm::Set(const char*))."""
+    torch = _torch()
+    _check_dev(base, "base", torch.uint8)
+    _check_dev(starts, "starts", torch.int64)
+    _check_dev(lens, "lens", torch.int64)
+    n = starts.numel()
+    h1 = torch.empty(n, dtype=torch.int64, device=base.device)
+    h2 = torch.empty(n, dtype=torch.int64, device=base.device) if second else None
+    flags = (FLAG_CSTR if cstr else 0) | (FLAG_STD_FNV if std_fnv else 0)
+    rc = _native.batch_lib().k2h_amd_hash_ranges(ctypes.c_void_p(base.data_ptr() or 1), _dev_ptr(starts),
+                                                 _dev_ptr(lens), n, _dev_ptr(h1),
+                                                 _dev_ptr(h2) if h2 is not None else None, flags,
+                                                 _stream_handle(stream))
+    _native.check(rc)
+    return h1, h2

@@ -406,6 +406,16 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* byt
   return K2H_AMD_OK;
 }
 
+__attribute__((visibility("default"))) int k2h_amd_hash_ranges(const void* base, const uint64_t* starts,
+                                                               const uint64_t* lens, uint64_t n, uint64_t* h1,
+                                                               uint64_t* h2, uint32_t flags, void* stream) {
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1 || !starts || !lens || !base) return fail(K2H_AMD_EINVAL, "NULL base/starts/lens/h1");
+  hipError_t e = k2h::launch_ranges(base, starts, lens, n, seed_for(flags), (flags & K2H_AMD_FLAG_CSTR) != 0, h1, h2,
+                                    variant(), (hipStream_t)stream);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_ranges", e);
+}
+
 // ---------------------------------------------------------------------------
 // RALLEDATA producer (include/k2hash_amd.h section 4)
 // ---------------------------------------------------------------------------

@@ -103,6 +103,10 @@ struct RalleInputs {
 hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, uint8_t* out, uint64_t* blob_off,
                             int variant, hipStream_t stream);
 
+// Keys at arbitrary (start, length) ranges (k2h_ranges.hip); cstr: hash key + NUL.
+hipError_t launch_ranges(const void* base, const uint64_t* starts, const uint64_t* lens, uint64_t n, uint64_t seed,
+                         bool cstr, uint64_t* h1, uint64_t* h2, int variant, hipStream_t stream);
+
 // S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).
 struct SpadTable {
   uint64_t v[16];
