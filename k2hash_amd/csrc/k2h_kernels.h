@@ -42,6 +42,9 @@ enum {
   kVariantFixed32Blk1024 = 26,
   kVariantFixed32Nt256 = 27,   // fixed32: the round-1 default (nt loads/stores, 256-thread blocks)
   kVariantRalleThread = 28,    // ralledata: one thread per record (default: 16 lanes per record)
+  kVariantFixed32W64Kpt2 = 29, // fixed32: one-wave blocks, 2 / 3 / 4 keys per lane, all loads issued first, nt
+  kVariantFixed32W64Kpt3 = 30,
+  kVariantFixed32W64Kpt4 = 31,
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with

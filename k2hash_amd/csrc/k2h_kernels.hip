@@ -251,24 +251,43 @@ __global__ __launch_bounds__(256) void fnv_fixed32_lds_kernel(const uint4* __res
 // fixed32, flat grid, KPT keys per thread: block b owns keys [b*256*KPT, (b+1)*256*KPT);
 // thread t hashes keys b*256*KPT + j*256 + t.  All 2*KPT loads are issued before the
 // first hash, so each wave keeps KPT*2 KiB in flight while it computes.
-template <bool H2, int KPT>
-__global__ __launch_bounds__(256) void fnv_fixed32_kpt_kernel(const uint4* __restrict__ keys, uint64_t n,
-                                                              uint64_t seed, uint64_t* __restrict__ h1,
-                                                              uint64_t* __restrict__ h2) {
-  const uint64_t base = (uint64_t)blockIdx.x * (256u * KPT) + threadIdx.x;
+template <bool H2, int KPT, int BS = 256, bool NT = false, bool EPI = false>
+__global__ __launch_bounds__(BS) void fnv_fixed32_kpt_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                             uint64_t seed, uint64_t* __restrict__ h1,
+                                                             uint64_t* __restrict__ h2, BucketParams bp = {}) {
+  const uint64_t base = (uint64_t)blockIdx.x * (BS * KPT) + threadIdx.x;
   uint4 a[KPT], b[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    uint64_t i = base + 256u * j;
+    uint64_t i = base + BS * j;
     if (i < n) {
-      a[j] = keys[2 * i];
-      b[j] = keys[2 * i + 1];
+      if constexpr (NT) {
+        a[j] = ld_nt(keys + 2 * i);
+        b[j] = ld_nt(keys + 2 * i + 1);
+      } else {
+        a[j] = keys[2 * i];
+        b[j] = keys[2 * i + 1];
+      }
     }
   }
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
-    uint64_t i = base + 256u * j;
-    if (i < n) fixed32_hash_store(a[j], b[j], seed, i, h1, h2, H2);
+    uint64_t i = base + BS * j;
+    if (i < n) {
+      if constexpr (NT) {
+        uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2, hi2;
+        if constexpr (H2) {
+          fnv_chunk32_last(lo, hi, lo2, hi2, a[j], b[j]);
+          st_nt(h2 + i, pack(lo2, hi2));
+        } else {
+          fnv_chunk32(lo, hi, a[j], b[j]);
+        }
+        st_nt(h1 + i, pack(lo, hi));
+        if constexpr (EPI) bucket_emit(bp, i, pack(lo, hi));
+      } else {
+        fixed32_hash_store(a[j], b[j], seed, i, h1, h2, H2);
+      }
+    }
   }
 }
 
@@ -426,23 +445,40 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
         else fnv_fixed32_kernel<false, false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
       case kVariantAuto: {
-        // one-wave blocks: a finished wave's slot is refilled at once instead of when the
-        // slowest of its block's four waves ends (3-4 % over 256-thread blocks, A/B in
-        // tools/variants.py, variants 0/23/24 of round 1)
-        unsigned g64 = (unsigned)((n + 63) / 64);
+        // One-wave blocks (a finished wave's slot is refilled at once instead of when the
+        // slowest of a block's four waves ends: 3-4 %), two keys per lane with all four
+        // loads issued before the first hash (a wave keeps 4 KiB in flight and half as
+        // many waves need dispatching: 5 % more).  Round-1 A/B, tools/variants.py,
+        // variants 0/23/27/29-31.  The second key's registers sit below the asm window,
+        // so the kernel stays at 59 VGPRs (8 waves/SIMD).
+        unsigned g = (unsigned)((n + 127) / 128);
         if (epi) {
-          if (h2) fnv_fixed32_kernel<true, true, true, true, 64><<<g64, 64, 0, stream>>>(k, n, seed, h1, h2, *bp);
-          else fnv_fixed32_kernel<false, true, true, true, 64><<<g64, 64, 0, stream>>>(k, n, seed, h1, nullptr, *bp);
+          if (h2) fnv_fixed32_kpt_kernel<true, 2, 64, true, true><<<g, 64, 0, stream>>>(k, n, seed, h1, h2, *bp);
+          else fnv_fixed32_kpt_kernel<false, 2, 64, true, true><<<g, 64, 0, stream>>>(k, n, seed, h1, nullptr, *bp);
           return hipGetLastError();
         }
-        if (h2) fnv_fixed32_kernel<true, true, true, false, 64><<<g64, 64, 0, stream>>>(k, n, seed, h1, h2);
-        else fnv_fixed32_kernel<false, true, true, false, 64><<<g64, 64, 0, stream>>>(k, n, seed, h1, nullptr);
+        if (h2) fnv_fixed32_kpt_kernel<true, 2, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_kpt_kernel<false, 2, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
       }
       case kVariantFixed32Nt256:
         if (h2) fnv_fixed32_kernel<true, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_kernel<false, true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
+      case kVariantFixed32W64Kpt2:
+      case kVariantFixed32W64Kpt3:
+      case kVariantFixed32W64Kpt4: {
+        const int kpt = variant == kVariantFixed32W64Kpt2 ? 2 : variant == kVariantFixed32W64Kpt3 ? 3 : 4;
+        unsigned g = (unsigned)((n + 64 * kpt - 1) / (64 * kpt));
+#define K2H_KPT(KK)                                                                                             \
+  if (h2) fnv_fixed32_kpt_kernel<true, KK, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, h2);                 \
+  else fnv_fixed32_kpt_kernel<false, KK, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, nullptr);
+        if (kpt == 2) { K2H_KPT(2) }
+        else if (kpt == 3) { K2H_KPT(3) }
+        else { K2H_KPT(4) }
+#undef K2H_KPT
+        break;
+      }
       case kVariantFixed32Blk64:
       case kVariantFixed32Blk128:
       case kVariantFixed32Blk512:
