@@ -71,6 +71,28 @@ __device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t src_lane) {
 __device__ __forceinline__ uint64_t bperm64(uint64_t v, uint32_t src_lane) {
   return ((uint64_t)bperm((uint32_t)(v >> 32), src_lane) << 32) | bperm((uint32_t)v, src_lane);
 }
+// LDS atomics and barriers for the phases that run while a tile's LDS-DMA is in flight.
+// hipcc (ROCm 7.2) puts an s_waitcnt vmcnt(0) in front of any LDS atomic and any
+// __syncthreads() while a global_load_lds is outstanding (it cannot prove they do not
+// alias the DMA target), which drained the whole tile DMA before the length sort
+// started.  As asm they carry no such wait; the sort touches only s_hist / s_order /
+// s_wsum, never the stage the DMA writes.
+__device__ __forceinline__ void lds_add(uint32_t* p, uint32_t v) {
+  asm volatile("ds_add_u32 %0, %1" ::"v"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)p), "v"(v)
+               : "memory");
+}
+__device__ __forceinline__ uint32_t lds_add_rtn(uint32_t* p, uint32_t v) {
+  uint32_t r;
+  asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)"
+               : "=v"(r)
+               : "v"((uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint32_t*)p), "v"(v)
+               : "memory");
+  return r;
+}
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
@@ -302,7 +324,7 @@ __device__ __forceinline__ uint32_t len_bin(uint64_t len) {
 // ---------------------------------------------------------------------------
 enum {
   kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
-  kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9
+  kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -312,11 +334,10 @@ enum {
     if (tid == 0) prof[(uint64_t)blockIdx.x * 16u + (SLOT)] = __builtin_amdgcn_s_memrealtime(); \
   }
 
-template <bool H2, int MODE, bool EPI = false>
-__global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __restrict__ bytes,
-                                                           const uint64_t* __restrict__ offsets, uint64_t n,
-                                                           SpadTable spad_tab, uint64_t* __restrict__ h1,
-                                                           uint64_t* __restrict__ h2, BucketParams bp = {}) {
+template <bool H2, int MODE, bool EPI>
+__device__ __forceinline__ void csr_tile(uint64_t tile, const uint8_t* __restrict__ bytes,
+                                         const uint64_t* __restrict__ offsets, uint64_t n, const SpadTable& spad_tab,
+                                         uint64_t* __restrict__ h1, uint64_t* __restrict__ h2, const BucketParams& bp) {
   __shared__ uint64_t s_off[kTileKeys + 1];
   __shared__ uint16_t s_order[kTileKeys];
   __shared__ uint32_t s_hist[kBins];
@@ -325,7 +346,7 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
   __shared__ TileLds s_u;
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint64_t t0 = (uint64_t)blockIdx.x * kTileKeys;
+  const uint64_t t0 = tile * kTileKeys;
   uint64_t* const prof = h2;  // profiling mode only: h2 is the stamp buffer (16 per block)
   (void)prof;
   K2H_PROF_STAMP(0)
@@ -366,10 +387,10 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
     uint32_t k = tid + 256u * j;
     if (k < cnt) {
       bins[j] = len_bin(s_off[k + 1] - s_off[k]);
-      atomicAdd(&s_hist[bins[j]], 1u);
+      lds_add(&s_hist[bins[j]], 1u);
     }
   }
-  __syncthreads();
+  lds_barrier();
   K2H_PROF_STAMP(11)
   // 2. exclusive scan of the 256 class counts (one per thread)
   uint32_t v = s_hist[tid], incl = v;
@@ -379,19 +400,19 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
     if (lane >= (uint32_t)d) incl += y;
   }
   if (lane == 63) s_wsum[wave] = incl;
-  __syncthreads();
+  lds_barrier();
   uint32_t base = 0;
   for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
   s_hist[tid] = base + incl - v;  // becomes the scatter cursor
-  __syncthreads();
+  lds_barrier();
   K2H_PROF_STAMP(12)
   // 3. scatter key indices in class order
 #pragma unroll
   for (int j = 0; j < kTileKeys / 256; ++j) {
     uint32_t k = tid + 256u * j;
-    if (k < cnt) s_order[atomicAdd(&s_hist[bins[j]], 1u)] = (uint16_t)k;
+    if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
   }
-  __syncthreads();
+  lds_barrier();
   // 4. each wave hashes groups of 64 class-sorted keys; results go straight to global
   //    (scattered 8-byte stores within the tile's 4 KiB output run merge in L2)
   K2H_PROF_STAMP(2)
@@ -401,7 +422,8 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
   }
   K2H_PROF_STAMP(3)
   // Groups are in length order, so wave w takes groups w, 7-w, 8+w, 15-w, ... (snake):
-  // every wave gets the same total work and the block's waves finish together.
+  // every wave gets the same total work and the block's waves finish together.  (Rotating
+  // the start by block, as the lean kernel does, measured 8 % slower here.)
   const uint32_t ngroups = (cnt + 63u) >> 6;
   for (uint32_t it = 0; it * 4 < ngroups; ++it) {
     uint32_t g = it * 4 + ((it & 1) ? 3 - wave : wave);
@@ -440,6 +462,32 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
   }
 }
 
+template <bool H2, int MODE, bool EPI = false>
+__global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __restrict__ bytes,
+                                                           const uint64_t* __restrict__ offsets, uint64_t n,
+                                                           SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                           uint64_t* __restrict__ h2, BucketParams bp = {}) {
+  csr_tile<H2, MODE, EPI>(blockIdx.x, bytes, offsets, n, spad_tab, h1, h2, bp);
+}
+
+// The tiles listed by the lean kernel as too large for its stage (tile_list[0 ..
+// *tile_count)), each hashed with the line ring; a grid-stride loop, since the count is
+// only known on the device.
+template <bool H2, bool EPI = false>
+__global__ __launch_bounds__(256) void fnv_csr_ring_list_kernel(const uint8_t* __restrict__ bytes,
+                                                                const uint64_t* __restrict__ offsets, uint64_t n,
+                                                                SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                                uint64_t* __restrict__ h2,
+                                                                const uint32_t* __restrict__ tile_list,
+                                                                const uint32_t* __restrict__ tile_count,
+                                                                BucketParams bp = {}) {
+  const uint32_t count = *tile_count;
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    csr_tile<H2, kModeRing, EPI>(tile_list[li], bytes, offsets, n, spad_tab, h1, h2, bp);
+    __syncthreads();  // the next tile reuses the shared arrays
+  }
+}
+
 // ---------------------------------------------------------------------------
 // CSR, lean staged tiles: TK keys per block of NW waves, the tile's bytes DMA'd into
 // an LDS stage of STAGE_KIB KiB with no line-ring union, so that several blocks fit a
@@ -459,11 +507,17 @@ __device__ __forceinline__ uint32_t len_bin128(uint64_t len) {
   return b < 128u ? b : 127u;
 }
 
-template <bool H2, int TK, int NW, int STAGE_KIB, int WALK = 1>
+// over_list / over_count (default path): a tile whose span exceeds the stage is not
+// hashed here but appended to over_list, for fnv_csr_ring_list_kernel; without a list
+// such tiles hash with per-lane direct loads (A/B variants).
+template <bool H2, int TK, int NW, int STAGE_KIB, int WALK = 1, bool EPI = false>
 __global__ __launch_bounds__(NW * 64) void fnv_csr_lean_kernel(const uint8_t* __restrict__ bytes,
                                                                const uint64_t* __restrict__ offsets, uint64_t n,
                                                                SpadTable spad_tab, uint64_t* __restrict__ h1,
-                                                               uint64_t* __restrict__ h2) {
+                                                               uint64_t* __restrict__ h2,
+                                                               uint32_t* __restrict__ over_list = nullptr,
+                                                               uint32_t* __restrict__ over_count = nullptr,
+                                                               BucketParams bp = {}) {
   constexpr int NT = NW * 64;
   constexpr int NB = 128;
   constexpr uint32_t kStage = STAGE_KIB * 1024u;
@@ -488,6 +542,10 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_lean_kernel(const uint8_t* __
   const uint64_t span_lo = ((uint64_t)(uintptr_t)bytes + s_off[0]) & ~15ull;
   const uint64_t span_hi = (uint64_t)(uintptr_t)bytes + s_off[cnt];
   const bool staged = span_hi - span_lo <= (uint64_t)kStage;
+  if (!staged && over_list) {  // block-uniform
+    if (tid == 0) over_list[atomicAdd(over_count, 1u)] = blockIdx.x;
+    return;
+  }
   if (staged) {
     const uint32_t npieces = s_off[cnt] > s_off[0] ? (uint32_t)((span_hi - span_lo + 1023) >> 10) : 0u;
     for (uint32_t c = wave; c < npieces; c += NW) {
@@ -504,10 +562,10 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_lean_kernel(const uint8_t* __
     uint32_t k = tid + NT * j;
     if (k < cnt) {
       bins[j] = len_bin128(s_off[k + 1] - s_off[k]);
-      atomicAdd(&s_hist[bins[j]], 1u);
+      lds_add(&s_hist[bins[j]], 1u);
     }
   }
-  __syncthreads();
+  lds_barrier();
   uint32_t v = tid < NB ? s_hist[tid] : 0u, incl = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
@@ -515,15 +573,15 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_lean_kernel(const uint8_t* __
     if (lane >= (uint32_t)d) incl += y;
   }
   if (lane == 63) s_wsum[wave] = incl;
-  __syncthreads();
+  lds_barrier();
   uint32_t base = 0;
   for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
   if (tid < NB) s_hist[tid] = base + incl - v;
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     uint32_t k = tid + NT * j;
-    if (k < cnt) s_order[atomicAdd(&s_hist[bins[j]], 1u)] = (uint16_t)k;
+    if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
   }
   if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -546,6 +604,7 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_lean_kernel(const uint8_t* __
     if (valid) {
       h1[t0 + k] = r1;
       if constexpr (H2) h2[t0 + k] = r2;
+      if constexpr (EPI) bucket_emit<false>(bp, t0 + k, r1);
     }
   }
 }
@@ -581,6 +640,97 @@ __global__ __launch_bounds__(256) void fnv_fixed_long_kernel(const uint8_t* __re
   if constexpr (EPI) bucket_emit(bp, i, r1);
 }
 
+// ---------------------------------------------------------------------------
+// Fixed-length keys of a multiple of 128 bytes from a 128-aligned base (BASELINE
+// config 5, 4 KiB): one lane per key; the keys are DMA'd into a per-wave LDS ring of D
+// rounds, round q = bytes [RB q, RB q + RB) of every lane's key (RB = 128: a whole line,
+// 64: half of one; 64 RB bytes per round), D-1 rounds in flight while the wave hashes
+// the current one.  No VGPR transit (global_load_lds), no per-chunk address math
+// (chunks are 16-aligned, so none straddles a round), and the DMA addresses are a
+// uniform base + fixed per-lane offsets.
+//
+// With NP = RB/16 pieces per round and LPI = 1024/RB lanes per DMA instruction,
+// instruction i of a round loads the pieces of lanes LPI i .. LPI i + LPI-1: lane t
+// fetches piece ((t % NP) + rot_L) % NP of lane L = LPI i + t / NP, rot_L =
+// (L / (256/RB)) % NP, into LDS byte 1024 i + 16 t.  Lane L's round then sits at
+// (L / LPI)*1024 + (L % LPI)*RB with piece j at position (j - rot_L) % NP, and when all
+// lanes read piece j together the 16 lanes of each ds_read_b128 pass hit 16 distinct
+// 4-bank groups (the row offset (L % LPI)*RB takes 256/RB bank phases, the rotation the
+// other NP).
+// ---------------------------------------------------------------------------
+// PROBE (timing probes only, wrong hashes): 1 = no DMA (hash whatever LDS holds),
+// 2 = no hashing (DMA + waits only).
+template <bool H2, int D, int RB, bool EPI = false, int PROBE = 0>
+__global__ __launch_bounds__(64) void fnv_fixed_lines_kernel(const uint8_t* __restrict__ base, uint64_t key_len,
+                                                             uint64_t n, uint64_t seed, uint64_t* __restrict__ h1,
+                                                             uint64_t* __restrict__ h2, BucketParams bp = {}) {
+  constexpr uint32_t NP = RB / 16, LPI = 1024 / RB, PH = 256 / RB;
+  static_assert((RB == 256 || RB == 128 || RB == 64) && D >= 2 && NP * (D - 1) <= 63,
+                "vmcnt holds at most 63 loads");
+  __shared__ __attribute__((aligned(1024))) uint8_t ring[D * 64 * RB];
+  const uint32_t t = threadIdx.x;
+  const uint64_t key0 = (uint64_t)blockIdx.x * 64u;
+  const uint32_t last = (uint32_t)(n - key0 < 64u ? n - key0 - 1 : 63u);  // highest lane holding a key
+  const uint32_t R = (uint32_t)(key_len / RB);                            // rounds per key (>= 1)
+  const uint32_t kl = (uint32_t)key_len;                                  // 64 * key_len < 2^32 (host check)
+
+  uint32_t voff[NP];
+#pragma unroll
+  for (uint32_t i = 0; i < NP; ++i) {
+    uint32_t L = LPI * i + t / NP;
+    uint32_t piece = ((t % NP) + (L / PH) % NP) % NP;
+    voff[i] = (L < last ? L : last) * kl + 16u * piece;  // lanes past the end re-read the last key
+  }
+  const uint32_t rot = (t / PH) % NP;
+  const uint32_t rowb = (t / LPI) * 1024u + (t % LPI) * RB;
+  uint32_t pofs[NP];
+#pragma unroll
+  for (uint32_t j = 0; j < NP; ++j) pofs[j] = rowb + 16u * ((j + NP - rot) % NP);
+  const uint8_t* wbase = base + key0 * key_len;
+
+  auto issue = [&](uint32_t q) {
+    if constexpr (PROBE == 1) return;
+    uint8_t* slot = ring + (q % D) * (64u * RB);
+    const uint8_t* src = wbase + (uint64_t)RB * q;
+#pragma unroll
+    for (uint32_t i = 0; i < NP; ++i)
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + voff[i]),
+                                       (__attribute__((address_space(3))) void*)(slot + 1024u * i), 16, 0, 0);
+  };
+
+  for (uint32_t q = 0; q < D - 1 && q < R; ++q) issue(q);
+  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2 = lo, hi2 = hi;
+  for (uint32_t q = 0; q < R; ++q) {
+    // slot (q+D-1) % D held round q-1, whose reads completed inside the previous round's
+    // asm statement (lgkmcnt(0) before its last chunk)
+    asm volatile("" ::: "memory");
+    if (q + D - 1 < R) {
+      issue(q + D - 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP * (D - 1)) : "memory");  // round q has landed
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // LDS reads in asm (fnv_lds_round): the compiler's own waits would drain every DMA
+    const uint32_t sb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(ring + (q % D) * (64u * RB));
+    uint32_t a[NP];
+#pragma unroll
+    for (uint32_t j = 0; j < NP; ++j) a[j] = sb + pofs[j];
+    if constexpr (PROBE == 2) {
+      lo ^= a[0];
+    } else if (q + 1 < R) {
+      fnv_lds_round<NP>(lo, hi, a);
+    } else {
+      fnv_lds_round_last<NP>(lo, hi, lo2, hi2, a);  // the state before the key's final byte
+    }
+  }
+  if (t > last) return;
+  const uint64_t i = key0 + t;
+  const uint64_t r1 = pack2(lo, hi);
+  __builtin_nontemporal_store(r1, h1 + i);
+  if constexpr (H2) __builtin_nontemporal_store(pack2(lo2, hi2), h2 + i);
+  if constexpr (EPI) bucket_emit(bp, i, r1);
+}
+
 // S_p = seed * P^-p mod 2^64, p = 0..15 (P = 1099511628211 is odd, so invertible).
 SpadTable make_spad(uint64_t seed) {
   const uint64_t P = 1099511628211ULL;
@@ -600,7 +750,41 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
   SpadTable t = make_spad(seed);
   unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
   const uint8_t* b = (const uint8_t*)bytes;
-  if (bp && mode == kModeStaged) {  // fused epilogue on the default kernel
+  if (mode == kModeLeanRing) {
+    // Default: 512-key tiles staged by the lean kernel (62 VGPRs, no ring code); tiles
+    // whose bytes exceed its 72 KiB stage are listed and hashed by the line-ring kernel
+    // in a second launch on the same stream (none for BASELINE config 3).
+    uint32_t* scratch = nullptr;  // [0] = count, [1..] = tile list
+    hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (g + 1), stream);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(scratch, 0, 4, stream);
+    const BucketParams none{};
+    const BucketParams& p = bp ? *bp : none;
+    const unsigned gl = g < 512u ? g : 512u;  // ring kernel: ~78 KiB LDS, two blocks per CU
+    if (e == hipSuccess) {
+      if (bp) {
+        if (h2) {
+          fnv_csr_lean_kernel<true, 512, 4, 72, 1, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, p);
+          fnv_csr_ring_list_kernel<true, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, p);
+        } else {
+          fnv_csr_lean_kernel<false, 512, 4, 72, 1, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, p);
+          fnv_csr_ring_list_kernel<false, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, p);
+        }
+      } else {
+        if (h2) {
+          fnv_csr_lean_kernel<true, 512, 4, 72><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+          fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+        } else {
+          fnv_csr_lean_kernel<false, 512, 4, 72><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+          fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+        }
+      }
+      e = hipGetLastError();
+    }
+    hipError_t f = hipFreeAsync(scratch, stream);
+    return e != hipSuccess ? e : f;
+  }
+  if (bp && mode == kModeStaged) {  // fused epilogue on the round-1 tile kernel
     if (h2) fnv_csr_tile_kernel<true, kModeStaged, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, *bp);
     else fnv_csr_tile_kernel<false, kModeStaged, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, *bp);
     return hipGetLastError();
@@ -645,12 +829,62 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
   return hipGetLastError();
 }
 
+bool fixed_lines_ok(const void* keys, uint64_t key_len) {
+  return key_len >= 128 && (key_len & 127u) == 0 && ((uintptr_t)keys & 127u) == 0 && key_len < (1ull << 26);
+}
+
 hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
-                             uint64_t* h2, bool direct, hipStream_t stream, const BucketParams* bp) {
+                             uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
+  const uint8_t* k = (const uint8_t*)keys;
+  if (mode == kLongAuto) mode = fixed_lines_ok(keys, key_len) ? kLongLines2 : kLongRing;
+  if (mode >= kLongLines2 && !fixed_lines_ok(keys, key_len)) mode = kLongRing;
+  if (mode >= kLongLines2) {
+    unsigned g = (unsigned)((n + 63) / 64);
+#define K2H_LINES(DD, RR)                                                                                         \
+  if (bp) {                                                                                                       \
+    if (h2) fnv_fixed_lines_kernel<true, DD, RR, true><<<g, 64, pad, stream>>>(k, key_len, n, seed, h1, h2, *bp);    \
+    else fnv_fixed_lines_kernel<false, DD, RR, true><<<g, 64, pad, stream>>>(k, key_len, n, seed, h1, nullptr, *bp); \
+  } else {                                                                                                          \
+    if (h2) fnv_fixed_lines_kernel<true, DD, RR><<<g, 64, pad, stream>>>(k, key_len, n, seed, h1, h2);               \
+    else fnv_fixed_lines_kernel<false, DD, RR><<<g, 64, pad, stream>>>(k, key_len, n, seed, h1, nullptr);            \
+  }
+    // kLongLines2Pad / Pad2: 4 / 2 KiB of dynamic LDS on top of the 16 KiB ring, i.e. 8 or
+    // 9 instead of 10 waves per CU (occupancy probes)
+    const unsigned pad = mode == kLongLines2Pad ? 4096u : mode == kLongLines2Pad2 ? 2048u : 0u;
+    if (mode >= kLongProbeCompute) {  // timing probes (wrong hashes)
+      if (mode == kLongProbeCompute)
+        fnv_fixed_lines_kernel<false, 2, 128, false, 1><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      else if (mode == kLongProbeMemory)
+        fnv_fixed_lines_kernel<false, 2, 128, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      else if (mode == kLongProbeMem3)
+        fnv_fixed_lines_kernel<false, 3, 128, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      else if (mode == kLongProbeMem4)
+        fnv_fixed_lines_kernel<false, 4, 128, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      else if (mode == kLongProbeMem256)
+        fnv_fixed_lines_kernel<false, 2, 256, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      else if (mode == kLongProbeMemHalf4)
+        fnv_fixed_lines_kernel<false, 4, 64, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      return hipGetLastError();
+    }
+    if (mode == kLongLines256 && key_len % 256 != 0) mode = kLongLines2;
+    if (mode == kLongLines256) {
+      K2H_LINES(2, 256)
+    } else
+    switch (mode) {
+      case kLongLines3: K2H_LINES(3, 128) break;
+      case kLongHalf5: K2H_LINES(5, 64) break;
+      case kLongHalf3: K2H_LINES(3, 64) break;
+      case kLongHalf4: K2H_LINES(4, 64) break;
+      case kLongHalf6: K2H_LINES(6, 64) break;
+      default: K2H_LINES(2, 128) break;
+    }
+#undef K2H_LINES
+    return hipGetLastError();
+  }
   SpadTable t = make_spad(seed);
   unsigned g = (unsigned)((n + 255) / 256);
-  const uint8_t* k = (const uint8_t*)keys;
-  if (bp && !direct) {  // fused epilogue on the default (line ring) kernel
+  const bool direct = mode == kLongDirect;
+  if (bp && !direct) {  // fused epilogue on the line ring kernel
     if (h2) fnv_fixed_long_kernel<true, false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2, *bp);
     else fnv_fixed_long_kernel<false, false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr, *bp);
     return hipGetLastError();

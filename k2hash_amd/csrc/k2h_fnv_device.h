@@ -280,3 +280,117 @@ __device__ __forceinline__ void fnv_lds_run(uint32_t& lo, uint32_t& hi, uint4& c
 }
 
 }  // namespace k2h
+
+// ---------------------------------------------------------------------------
+// Eight 16-byte chunks read from LDS at per-lane addresses a[0..7] (one line of a key),
+// hashed in order as ONE asm statement: reads alternate between v[40:43] and v[44:47],
+// the next chunk's ds_read_b128 is in flight under the current chunk's steps, and the
+// lgkmcnt waits are explicit -- the compiler's own wait insertion would otherwise
+// treat every LDS read as aliasing the LDS-DMA loads still in flight and drain them
+// all (s_waitcnt vmcnt(0)) before the first read.  LAST: the eighth chunk is the key's
+// final one and its pre-final-byte state (the second hash) is returned in lo2/hi2.
+// ---------------------------------------------------------------------------
+namespace k2h {
+
+#define K2H_R8_BODY(LASTCHUNK)                                               \
+  "ds_read_b128 v[40:43], %[a0]\n\t"                                         \
+  "ds_read_b128 v[44:47], %[a1]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "ds_read_b128 v[40:43], %[a2]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_B                                   \
+  "ds_read_b128 v[44:47], %[a3]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "ds_read_b128 v[40:43], %[a4]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_B                                   \
+  "ds_read_b128 v[44:47], %[a5]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "ds_read_b128 v[40:43], %[a6]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_B                                   \
+  "ds_read_b128 v[44:47], %[a7]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "s_waitcnt lgkmcnt(0)\n\t" LASTCHUNK
+
+#define K2H_R8_INPUTS                                                                                        \
+  [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [a4] "v"(a[4]), [a5] "v"(a[5]),              \
+      [a6] "v"(a[6]), [a7] "v"(a[7]), "{v50}"(0u), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+#define K2H_R8_CLOBBERS                                                                                      \
+  "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v51", "v52", "v53", "v54", "v56", "v57", "v58", "vcc", \
+      "memory"
+
+#define K2H_R4_BODY(LASTCHUNK)                                               \
+  "ds_read_b128 v[40:43], %[a0]\n\t"                                         \
+  "ds_read_b128 v[44:47], %[a1]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "ds_read_b128 v[40:43], %[a2]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_B                                   \
+  "ds_read_b128 v[44:47], %[a3]\n\t"                                         \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "s_waitcnt lgkmcnt(0)\n\t" LASTCHUNK
+#define K2H_R4_INPUTS                                                                                        \
+  [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), "{v50}"(0u), [p] "s"(kPrimeLo),             \
+      [sel] "s"(kSmearSel)
+#define K2H_LAST_B K2H_X_PAIR("v44", "v45", "v[44:45]") K2H_X_PAIR_LAST("v46", "v47", "v[46:47]")
+
+// NP = 8 or 4 chunks per round (a full 128-byte line, or half of one).
+template <int NP>
+__device__ __forceinline__ void fnv_lds_round(uint32_t& lo, uint32_t& hi, const uint32_t (&a)[NP]);
+
+// NP = 16 (two lines per round): two eight-chunk statements.
+__device__ __forceinline__ void fnv_lds_round16(uint32_t& lo, uint32_t& hi, const uint32_t (&a16)[16], bool last,
+                                                uint32_t& lo2, uint32_t& hi2) {
+  {
+    const uint32_t(&a)[8] = *reinterpret_cast<const uint32_t(*)[8]>(&a16[0]);
+    asm volatile(K2H_R8_BODY(K2H_X_CHUNK_B) : "+{v48}"(lo), "+{v49}"(hi) : K2H_R8_INPUTS : K2H_R8_CLOBBERS);
+  }
+  const uint32_t(&a)[8] = *reinterpret_cast<const uint32_t(*)[8]>(&a16[8]);
+  if (!last) {
+    asm volatile(K2H_R8_BODY(K2H_X_CHUNK_B) : "+{v48}"(lo), "+{v49}"(hi) : K2H_R8_INPUTS : K2H_R8_CLOBBERS);
+  } else {
+    asm volatile(K2H_R8_BODY(K2H_LAST_B)
+                 : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2)
+                 : K2H_R8_INPUTS
+                 : K2H_R8_CLOBBERS);
+  }
+}
+
+template <int NP>
+__device__ __forceinline__ void fnv_lds_round(uint32_t& lo, uint32_t& hi, const uint32_t (&a)[NP]) {
+  if constexpr (NP == 16) {
+    uint32_t d0, d1;
+    fnv_lds_round16(lo, hi, a, false, d0, d1);
+  } else if constexpr (NP == 8)
+    asm volatile(K2H_R8_BODY(K2H_X_CHUNK_B) : "+{v48}"(lo), "+{v49}"(hi) : K2H_R8_INPUTS : K2H_R8_CLOBBERS);
+  else
+    asm volatile(K2H_R4_BODY(K2H_X_CHUNK_B) : "+{v48}"(lo), "+{v49}"(hi) : K2H_R4_INPUTS : K2H_R8_CLOBBERS);
+}
+
+template <int NP>
+__device__ __forceinline__ void fnv_lds_round_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2,
+                                                   const uint32_t (&a)[NP]) {
+  if constexpr (NP == 16)
+    fnv_lds_round16(lo, hi, a, true, lo2, hi2);
+  else if constexpr (NP == 8)
+    asm volatile(K2H_R8_BODY(K2H_LAST_B)
+                 : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2)
+                 : K2H_R8_INPUTS
+                 : K2H_R8_CLOBBERS);
+  else
+    asm volatile(K2H_R4_BODY(K2H_LAST_B)
+                 : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2)
+                 : K2H_R4_INPUTS
+                 : K2H_R8_CLOBBERS);
+}
+
+__device__ __forceinline__ void fnv_lds_round8(uint32_t& lo, uint32_t& hi, const uint32_t (&a)[8]) {
+  asm volatile(K2H_R8_BODY(K2H_X_CHUNK_B) : "+{v48}"(lo), "+{v49}"(hi) : K2H_R8_INPUTS : K2H_R8_CLOBBERS);
+}
+
+__device__ __forceinline__ void fnv_lds_round8_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2,
+                                                    const uint32_t (&a)[8]) {
+  asm volatile(K2H_R8_BODY(K2H_X_PAIR("v44", "v45", "v[44:45]") K2H_X_PAIR_LAST("v46", "v47", "v[46:47]"))
+               : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2)
+               : K2H_R8_INPUTS
+               : K2H_R8_CLOBBERS);
+}
+
+}  // namespace k2h

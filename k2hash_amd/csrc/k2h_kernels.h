@@ -45,6 +45,23 @@ enum {
   kVariantFixed32W64Kpt2 = 29, // fixed32: one-wave blocks, 2 / 3 / 4 keys per lane, all loads issued first, nt
   kVariantFixed32W64Kpt3 = 30,
   kVariantFixed32W64Kpt4 = 31,
+  kVariantLongRing = 32,       // fixed long keys: the cooperative line ring (the round-1 kernel)
+  kVariantLongLines2 = 33,     // fixed long keys (len % 128 == 0): line DMA into a 2 / 3-round LDS ring
+  kVariantLongLines3 = 34,
+  kVariantLongHalf3 = 35,      // ... half-line rounds (64 B per lane), 3 / 4 / 6 of them
+  kVariantLongHalf4 = 36,
+  kVariantLongHalf6 = 37,
+  kVariantLongHalf5 = 38,      // ... 5 half-line rounds (20 KiB: 8 waves per CU)
+  kVariantLongLines2Pad = 39,  // 2 line rounds + 4 KiB / 2 KiB of LDS padding (8 / 9 waves per CU)
+  kVariantLongLines2Pad2 = 40,
+  kVariantLongProbeCompute = 41,  // timing probes (WRONG hashes): line-DMA kernel without DMA / without hashing
+  kVariantLongProbeMemory = 42,
+  kVariantLongProbeMem3 = 43,     // DMA-only probes at 3 / 4 line rounds, 2 double-line rounds, 4 half-line rounds
+  kVariantLongProbeMem4 = 44,
+  kVariantLongProbeMem256 = 45,
+  kVariantLongProbeMemHalf4 = 46,
+  kVariantLongLines256 = 47,
+  kVariantCsrTile = 48,           // csr: the round-1 default (512-key tile kernel with the ring inside)      // fixed long keys (len % 256 == 0): 2 rounds of 256 B per lane (32 KiB)
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with
@@ -119,8 +136,19 @@ SpadTable make_spad(uint64_t seed);
 // mode: 0 = tile staged in LDS by DMA (ring for oversize tiles), 1 = per-lane direct, 2 = ring only
 hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp = nullptr);
+// Long fixed-length keys: mode kLongAuto picks the line-DMA kernel (key_len % 128 == 0,
+// 128-aligned keys; 2 rounds of whole lines), else the cooperative line ring.
+// kLongHalfD: rounds of half lines (64 B per lane), D of them.
+enum { kLongAuto = 0, kLongDirect = 1, kLongRing = 2, kLongLines2 = 3, kLongLines3 = 4, kLongHalf3 = 5,
+       kLongHalf4 = 6, kLongHalf6 = 7, kLongHalf5 = 8, kLongLines2Pad = 9, kLongLines2Pad2 = 10,
+       kLongLines256 = 11,
+       // timing probes (wrong hashes), keep last: no DMA / DMA only at (D, RB) =
+       // (2,128) (2,128) (3,128) (4,128) (2,256) (4,64)
+       kLongProbeCompute = 12, kLongProbeMemory = 13, kLongProbeMem3 = 14, kLongProbeMem4 = 15,
+       kLongProbeMem256 = 16, kLongProbeMemHalf4 = 17 };
+bool fixed_lines_ok(const void* keys, uint64_t key_len);
 hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
-                             uint64_t* h2, bool direct, hipStream_t stream, const BucketParams* bp = nullptr);
+                             uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp = nullptr);
 
 hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
                         int variant, hipStream_t stream, const BucketParams* bp = nullptr);

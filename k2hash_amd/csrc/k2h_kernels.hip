@@ -548,9 +548,30 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
   // Routing by key length (tools/fixed_sweep.py on MI355X, 512 MiB of keys per launch):
   // up to 32 B the per-lane tail loop is fastest, below 128 B per-lane direct 16-byte
   // loads, from 128 B on the cooperative line ring.
+  // From 128 B on, keys of a multiple of 128 bytes at a 128-aligned base take the line-DMA
+  // kernel, everything else the cooperative line ring.
   if (variant == kVariantAuto) variant = key_len <= 32 ? kVariantFixedTail : key_len < 128 ? kVariantDirect : 0;
-  if (variant != kVariantFixedTail)
-    return launch_fixed_long(keys, key_len, n, seed, h1, h2, variant == kVariantDirect, stream, epi ? bp : nullptr);
+  if (variant != kVariantFixedTail) {
+    const int mode = variant == kVariantDirect       ? kLongDirect
+                     : variant == kVariantLongRing   ? kLongRing
+                     : variant == kVariantLongLines2 ? kLongLines2
+                     : variant == kVariantLongLines3 ? kLongLines3
+                     : variant == kVariantLongHalf3  ? kLongHalf3
+                     : variant == kVariantLongHalf4  ? kLongHalf4
+                     : variant == kVariantLongHalf6  ? kLongHalf6
+                     : variant == kVariantLongHalf5  ? kLongHalf5
+                     : variant == kVariantLongLines2Pad ? kLongLines2Pad
+                     : variant == kVariantLongLines2Pad2 ? kLongLines2Pad2
+                     : variant == kVariantLongProbeCompute ? kLongProbeCompute
+                     : variant == kVariantLongProbeMemory ? kLongProbeMemory
+                     : variant == kVariantLongProbeMem3 ? kLongProbeMem3
+                     : variant == kVariantLongProbeMem4 ? kLongProbeMem4
+                     : variant == kVariantLongProbeMem256 ? kLongProbeMem256
+                     : variant == kVariantLongProbeMemHalf4 ? kLongProbeMemHalf4
+                     : variant == kVariantLongLines256 ? kLongLines256
+                                                     : kLongAuto;
+    return launch_fixed_long(keys, key_len, n, seed, h1, h2, mode, stream, epi ? bp : nullptr);
+  }
   const uint8_t* kb = (const uint8_t*)keys;
   if (epi) {
     if (h2) fnv_fixed_kernel<true, true><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, h2, *bp);
@@ -629,7 +650,8 @@ hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, ui
                          : variant == kVariantCsrLean512x8 ? 7
                          : variant == kVariantCsrLean512x4 ? 8
                          : variant == kVariantCsrAlignProbe ? 9
-                                                        : 0,
+                         : variant == kVariantCsrTile   ? 0
+                                                        : 10,
                          stream, epi ? bp : nullptr);
 }
 

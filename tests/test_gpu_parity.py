@@ -17,7 +17,7 @@ from k2hash_amd import batch
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12, 16, 17, 18, 23, 24, 25, 26, 27, 29, 30, 31]
-CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21]
+CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21, 48]
 
 
 def dev_u8(torch, arr, device, pad_front=0):
@@ -218,7 +218,7 @@ def test_full_size_fixed_digest(cuda, oracle, digests, name):
     assert torch.equal(g1, h1)
 
 
-@pytest.mark.parametrize("variant", [0, 19, 20, 21])
+@pytest.mark.parametrize("variant", [0, 19, 20, 21, 48])
 @pytest.mark.parametrize("name", ["csr_8_256_64M", "csr_8_256_64K"])
 def test_full_size_csr_digest(cuda, oracle, digests, name, variant):
     import torch
@@ -242,3 +242,22 @@ def test_config4_shard_digests(cuda, oracle, digests):
         torch.cuda.synchronize()
         _check_digest(oracle, cfg, h1, h2, first=c["first"], expect=c)
         del keys, h1, h2
+
+
+@pytest.mark.parametrize("variant", [32, 33, 34, 35, 36, 37, 38, 39, 40, 47])
+@pytest.mark.parametrize("key_len,n", [(128, 1), (128, 64), (256, 517), (384, 130), (1024, 200), (4096, 67)])
+def test_fixed_long_kernels_vs_oracle(cuda, oracle, variant, key_len, n):
+    """Long fixed-length keys: the line ring (32) and the line-DMA ring kernels (33-35,
+    2/3/4 rounds), partial last waves included; h1 and h2."""
+    import torch
+    data = oracle.gen_bytes(key_len * n, byte_off=3 * key_len + 1)
+    r1, r2 = oracle.hash_fixed(data, key_len)
+    batch.set_variant(variant)
+    keys = dev_u8(torch, data, cuda)
+    assert keys.data_ptr() % 128 == 0
+    h1, h2 = k2hash_amd.hash_fixed(keys, key_len, second=True)
+    g1, _ = k2hash_amd.hash_fixed(keys, key_len)
+    torch.cuda.synchronize()
+    assert np.array_equal(host_u64(h1), r1)
+    assert np.array_equal(host_u64(h2), r2)
+    assert np.array_equal(host_u64(g1), r1)
