@@ -162,7 +162,7 @@ def main():
         if kind == "ralledata":
             from k2hash_amd import ralledata
             (kd, ko, vd, vo), (blob, boff) = keys, off
-            ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff)
+            ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff, total=blob.numel())
             return
         if args.index:
             import ctypes

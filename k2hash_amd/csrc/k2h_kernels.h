@@ -61,7 +61,9 @@ enum {
   kVariantLongProbeMem256 = 45,
   kVariantLongProbeMemHalf4 = 46,
   kVariantLongLines256 = 47,
-  kVariantCsrTile = 48,           // csr: the round-1 default (512-key tile kernel with the ring inside)      // fixed long keys (len % 256 == 0): 2 rounds of 256 B per lane (32 KiB)
+  kVariantCsrTile = 48,           // csr: the round-1 default (512-key tile kernel with the ring inside)
+  kVariantRalleGroup16 = 49,      // ralledata: 16 lanes per record (default 8), overlapped 16-byte tails
+  kVariantRalleByteTail = 50,     // ralledata: the round-1 assembly (16 lanes, tails one byte per lane)      // fixed long keys (len % 256 == 0): 2 rounds of 256 B per lane (32 KiB)
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with

@@ -69,26 +69,35 @@ __global__ __launch_bounds__(256) void ralledata_assemble_kernel(RalleInputs in,
   }
 }
 
-// Group form (default): 16 lanes per record, 4 records per wave.  Lane q of a group
-// writes header piece q (5 x 16 B) and copies bytes [16q + 256j, +16) of each segment,
-// so a group's loads and stores are consecutive 16-byte pieces (256 B per instruction
-// per group) instead of one lane streaming a whole record; the last partial piece of a
-// segment is copied one byte per lane.
-constexpr int kGroup = 16;
-
+// Group form (default): G lanes per record, 64/G records per wave.  Lane q of a group
+// writes header piece q (5 x 16 B) and copies bytes [16q + 16Gj, +16) of each segment,
+// so a group's loads and stores are consecutive 16-byte pieces instead of one lane
+// streaming a whole record.  A segment's last partial piece is the 16 bytes ENDING at
+// its last byte (they overlap the previous piece with the same bytes, so the order of
+// the two stores does not matter); only segments shorter than 16 bytes are copied byte
+// by byte.  G = 8 keeps most lanes busy on BASELINE-like records (keys 8-64 B, values
+// 0-256 B); G = 16 and the round-1 byte-tail form are A/B variants.
+template <int G, bool BYTE_TAIL = false>
 __device__ __forceinline__ void group_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len,
                                            uint32_t q) {
   uint64_t full = len & ~15ull;
-  for (uint64_t j = 16ull * q; j < full; j += 16ull * kGroup)
+  for (uint64_t j = 16ull * q; j < full; j += 16ull * G)
     *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
-  uint64_t t = full + q;  // the <= 15 tail bytes: one byte per lane, one instruction
-  if (t < len) dst[t] = src[t];
+  if (full == len) return;
+  if (!BYTE_TAIL && len >= 16) {
+    if (q == G - 1)
+      *reinterpret_cast<u32x4_ua*>(dst + len - 16) = *reinterpret_cast<const u32x4_ua*>(src + len - 16);
+    return;
+  }
+  for (uint64_t t = full + q; t < len; t += G) dst[t] = src[t];  // the <= 15 tail bytes
 }
 
+template <int G, bool BYTE_TAIL = false>
 __global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
                                                               uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
-  const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / kGroup;
-  const uint32_t q = threadIdx.x % kGroup;
+  static_assert(G >= 5 && 64 % G == 0, "five lanes write the header");
+  const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / G;
+  const uint32_t q = threadIdx.x % G;
   if (i >= n) return;
   const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i), al = seg_len(in.aoff, i);
   const uint64_t o = 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) +
@@ -106,10 +115,10 @@ __global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, ui
     *reinterpret_cast<u32x4_ua*>(b + 16 * q) =
         u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
   }
-  if (kl) group_copy(b + 80, in.keys + in.koff[i], kl, q);
-  if (vl) group_copy(b + 80 + kl, in.vals + in.voff[i], vl, q);
-  if (sl) group_copy(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
-  if (al) group_copy(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
+  if (kl) group_copy<G, BYTE_TAIL>(b + 80, in.keys + in.koff[i], kl, q);
+  if (vl) group_copy<G, BYTE_TAIL>(b + 80 + kl, in.vals + in.voff[i], vl, q);
+  if (sl) group_copy<G, BYTE_TAIL>(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
+  if (al) group_copy<G, BYTE_TAIL>(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
   if (blob_off && q == 0) {
     blob_off[i] = o;
     if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
@@ -131,8 +140,12 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
   if (e == hipSuccess) {
     if (variant == kVariantRalleThread)
       ralledata_assemble_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else if (variant == kVariantRalleGroup16)
+      ralledata_group_kernel<16><<<(unsigned)((n * 16 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else if (variant == kVariantRalleByteTail)
+      ralledata_group_kernel<16, true><<<(unsigned)((n * 16 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     else
-      ralledata_group_kernel<<<(unsigned)((n * kGroup + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+      ralledata_group_kernel<8><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     e = hipGetLastError();
   }
   hipError_t f = hipFreeAsync(h, stream);

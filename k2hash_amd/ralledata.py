@@ -50,9 +50,13 @@ def _seg_bytes(off) -> int:
 
 
 def build_ralledata(keys, key_off, vals=None, val_off=None, skeys=None, skey_off=None, attrs=None, attr_off=None,
-                    std_fnv: bool = False, out=None, blob_off=None, stream=None):
+                    std_fnv: bool = False, out=None, blob_off=None, stream=None, total: Optional[int] = None):
     """Device form.  Each segment is (uint8 bytes tensor, int64 offsets tensor of n+1) or
-    (None, None).  Returns (blobs uint8 tensor, blob_off int64 tensor of n+1)."""
+    (None, None).  Returns (blobs uint8 tensor, blob_off int64 tensor of n+1).
+
+    The blob size is computed from the first and last offset of every segment, which
+    reads them back from the device (a stream sync); a caller that already knows it
+    (`ralledata_size`) passes `total` together with `out` and the call stays async."""
     torch = _torch()
     _check_dev(key_off, "key_off", torch.int64)
     n = key_off.numel() - 1
@@ -67,8 +71,11 @@ def build_ralledata(keys, key_off, vals=None, val_off=None, skeys=None, skey_off
         _check_dev(o, f"{name} offsets", torch.int64)
         _check_dev(b, name, torch.uint8)
         args += [ctypes.c_void_p(b.data_ptr() or 1), _dev_ptr(o)]
-        nbytes.append(_seg_bytes(o))
-    total = ralledata_size(n, *nbytes)
+        nbytes.append(0 if total is not None and out is not None else _seg_bytes(o))
+    if total is None or out is None:
+        total = ralledata_size(n, *nbytes)
+    elif out.numel() < total:
+        raise ValueError("out is smaller than total")
     dev = key_off.device
     if out is None:
         out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
