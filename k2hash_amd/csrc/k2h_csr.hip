@@ -324,7 +324,8 @@ __device__ __forceinline__ uint32_t len_bin(uint64_t len) {
 // ---------------------------------------------------------------------------
 enum {
   kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
-  kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10
+  kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10,
+  kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -610,6 +611,216 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_lean_kernel(const uint8_t* __
 }
 
 // ---------------------------------------------------------------------------
+// CSR lean tiles, trimmed of non-hash VALU work (the kernel is bound by its VALU
+// instruction count): 32-bit tile-relative offsets in LDS, a DMA
+// loop with one 32-bit clamp per piece and a wave-uniform trip count, and the chunk-0
+// lead mask from a 16-entry table.  Same tile
+// shape as fnv_csr_lean_kernel<512, 4, 72>; oversize tiles go to the ring list.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t len_bin128_32(uint32_t len) {
+  if (len == 0) return 0;
+  uint32_t k = (len + 15u) >> 4;
+  if (k < 96) return k;
+  uint32_t lg = 31u - (uint32_t)__clz((int)k);  // >= 6
+  uint32_t b = 96u + (lg - 6u) * 4u + ((k >> (lg - 2u)) & 3u);
+  return b < 128u ? b : 127u;
+}
+
+// Key [rs, re) of the tile (byte offsets relative to the tile's first key byte, which
+// sits at `key0` in LDS; 16 readable bytes precede the stage for chunk 0's pad).
+template <bool PIN>
+__device__ __forceinline__ void lds_hash32(bool valid, uint32_t rs, uint32_t re, const uint8_t* key0,
+                                           const uint64_t* spad, const uint4* masks, uint64_t& r1,
+                                           uint64_t& r2) {
+  const uint32_t len = valid ? re - rs : 0u;
+  const uint32_t k = (len + 15u) >> 4;
+  const uint32_t p = (0u - len) & 15u;
+  const uint8_t* cp = key0 + (int32_t)(re - 16u * k);  // chunk 0 (idle lanes: harmless reads)
+  const uint64_t st = spad[p];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2 = lo, hi2 = hi;
+  const uint4 m = masks[p];
+  uint4 c0 = ld16(cp);
+  c0 = make_uint4(c0.x & m.x, c0.y & m.y, c0.z & m.z, c0.w & m.w);
+  // PIN (A/B): pin the chunk registers to the asm banks (v[40:43] / v[44:47]) so the LDS
+  // reads land there directly -- but the pin waits for each read (lgkmcnt(0)) right
+  // after issuing it, which costs more than the copies it saves
+  auto pin0 = [](uint4& c) {
+    if constexpr (PIN) asm volatile("" : "+{v40}"(c.x), "+{v41}"(c.y), "+{v42}"(c.z), "+{v43}"(c.w));
+  };
+  auto pin1 = [](uint4& c) {
+    if constexpr (PIN) asm volatile("" : "+{v44}"(c.x), "+{v45}"(c.y), "+{v46}"(c.z), "+{v47}"(c.w));
+  };
+  pin0(c0);
+  uint4 c1 = c0;
+  bool odd = false;
+  for (uint32_t j = 0; j + 1 < k; j += 2) {
+    c1 = ld16(cp + 16u * (j + 1));
+    pin1(c1);
+    fnv_chunk16<0>(lo, hi, c0);
+    if (j + 2 >= k) {
+      odd = true;
+      break;
+    }
+    c0 = ld16(cp + 16u * (j + 2));
+    pin0(c0);
+    fnv_chunk16<1>(lo, hi, c1);
+  }
+  if (odd) c0 = c1;
+  fnv_chunk16_last(lo, hi, lo2, hi2, c0);
+  if (k == 0) {
+    r1 = r2 = 0;
+    return;
+  }
+  r1 = pack2(lo, hi);
+  r2 = len == 1 ? r1 : pack2(lo2, hi2);
+}
+
+// The same walk with the chunk registers held in the asm banks across the loop
+// (fnv_step_read: each step hashes one bank while its asm reads the next chunk into the
+// other): no copies in the loop (≈3 fewer VALU ops per chunk), yet 3 % slower than the
+// compiler-scheduled walk in A/B (variant 53), so it is not the default.
+__device__ __forceinline__ void lds_hash32s(bool valid, uint32_t rs, uint32_t re, const uint8_t* key0,
+                                            const uint64_t* spad, const uint4* masks, uint64_t& r1, uint64_t& r2) {
+  const uint32_t len = valid ? re - rs : 0u;
+  const uint32_t k = (len + 15u) >> 4;
+  const uint32_t p = (0u - len) & 15u;
+  const uint8_t* cp = key0 + (int32_t)(re - 16u * k);
+  const uint64_t st = spad[p];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2 = lo, hi2 = hi;
+  const uint4 m = masks[p];
+  uint4 a = ld16(cp);
+  a = make_uint4(a.x & m.x, a.y & m.y, a.z & m.z, a.w & m.w);
+  fnv_bank0_pin(a);
+  uint4 b = a;
+  const uint32_t a0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint8_t*)cp;
+  bool from1 = false;
+  for (uint32_t j = 0; j + 1 < k; j += 2) {
+    fnv_step_read<0>(lo, hi, a, b, a0 + 16u * (j + 1));
+    if (j + 2 >= k) {
+      from1 = true;
+      break;
+    }
+    fnv_step_read<1>(lo, hi, a, b, a0 + 16u * (j + 2));
+  }
+  fnv_step_last(lo, hi, lo2, hi2, a, b, from1);
+  if (k == 0) {
+    r1 = r2 = 0;
+    return;
+  }
+  r1 = pack2(lo, hi);
+  r2 = len == 1 ? r1 : pack2(lo2, hi2);
+}
+
+template <bool H2, bool EPI = false, int WALK = 0>
+__global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
+                                                            const uint64_t* __restrict__ offsets, uint64_t n,
+                                                            SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                            uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
+                                                            uint32_t* __restrict__ over_count, BucketParams bp = {}) {
+  constexpr uint32_t TK = 512, NW = 4, NT = 256, NB = 128;
+  constexpr uint32_t kStage = 72 * 1024u;
+  __shared__ uint32_t s_rel[TK + 1];
+  __shared__ uint16_t s_order[TK];
+  __shared__ uint32_t s_hist[NB];
+  __shared__ uint32_t s_wsum[NW];
+  __shared__ uint64_t s_spad[16];
+  __shared__ uint4 s_mask[16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[16 + kStage];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t t0 = (uint64_t)blockIdx.x * TK;
+  const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
+  const uint64_t o0 = offsets[t0], oN = offsets[t0 + cnt];  // block-uniform
+  const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
+  const uint64_t span_lo = kb & ~15ull;
+  const uint32_t delta = (uint32_t)(kb & 15u);
+  const uint64_t span = oN - o0 + delta;  // stage bytes up to the tile's last key byte
+  if (span > kStage) {                    // block-uniform
+    if (tid == 0) over_list[atomicAdd(over_count, 1u)] = blockIdx.x;
+    return;
+  }
+  if (tid < 16) {
+    s_spad[tid] = spad_tab.v[tid];
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
+      int32_t sh = 8 * ((int32_t)tid - 4 * i);
+      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
+    }
+    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  for (uint32_t k = tid; k <= cnt; k += NT) s_rel[k] = (uint32_t)(offsets[t0 + k] - o0);
+  if (tid < NB) s_hist[tid] = 0;
+  __syncthreads();
+
+  // DMA of the tile span (16-byte pieces; pieces past the span re-read its last piece
+  // into stage bytes nobody reads), in flight during the sort
+  if (oN > o0) {
+    const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
+    const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
+    const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
+    uint32_t off = 1024u * wave + 16u * lane;
+    for (uint32_t c = wave; c < npieces; c += NW, off += 1024u * NW) {
+      const uint32_t o = off < lastp ? off : lastp;
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
+                                       (__attribute__((address_space(3))) void*)(s_stage + 16 + 1024u * c), 16, 0, 0);
+    }
+  }
+  constexpr uint32_t KPT = (TK + NT - 1) / NT;
+  uint32_t bins[KPT];
+#pragma unroll
+  for (uint32_t j = 0; j < KPT; ++j) {
+    uint32_t k = tid + NT * j;
+    if (k < cnt) {
+      bins[j] = len_bin128_32(s_rel[k + 1] - s_rel[k]);
+      lds_add(&s_hist[bins[j]], 1u);
+    }
+  }
+  lds_barrier();
+  uint32_t v = tid < NB ? s_hist[tid] : 0u, incl = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(incl, d, 64);
+    if (lane >= (uint32_t)d) incl += y;
+  }
+  if (lane == 63) s_wsum[wave] = incl;
+  lds_barrier();
+  uint32_t base = 0;
+  for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
+  if (tid < NB) s_hist[tid] = base + incl - v;
+  lds_barrier();
+#pragma unroll
+  for (uint32_t j = 0; j < KPT; ++j) {
+    uint32_t k = tid + NT * j;
+    if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces have landed
+  __syncthreads();                                   // ... and every other wave's
+
+  const uint8_t* key0 = s_stage + 16 + delta;
+  const uint32_t ngroups = (cnt + 63u) >> 6;
+  const uint32_t wr = (wave + blockIdx.x) % NW;
+  for (uint32_t it = 0; it * NW < ngroups; ++it) {
+    uint32_t g = it * NW + ((it & 1) ? NW - 1 - wr : wr);
+    if (g >= ngroups) continue;
+    uint32_t idx = g * 64u + lane;
+    bool valid = idx < cnt;
+    uint32_t k = s_order[valid ? idx : cnt - 1];
+    uint64_t r1, r2;
+    if constexpr (WALK == 2)
+      lds_hash32s(valid, s_rel[k], s_rel[k + 1], key0, s_spad, s_mask, r1, r2);
+    else
+      lds_hash32<WALK == 1>(valid, s_rel[k], s_rel[k + 1], key0, s_spad, s_mask, r1, r2);
+    if (valid) {
+      h1[t0 + k] = r1;
+      if constexpr (H2) h2[t0 + k] = r2;
+      if constexpr (EPI) bucket_emit<false>(bp, t0 + k, r1);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Fixed-length keys other than the 32-byte fast path (e.g. BASELINE config 5,
 // 4 KiB): one lane per key, the same chunk walker, uniform trip count.
 // ---------------------------------------------------------------------------
@@ -750,7 +961,7 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
   SpadTable t = make_spad(seed);
   unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
   const uint8_t* b = (const uint8_t*)bytes;
-  if (mode == kModeLeanRing) {
+  if (mode == kModeLeanRing || mode == kModeLean2Ring || mode == kModeLean2Pin || mode == kModeLean2Step) {
     // Default: 512-key tiles staged by the lean kernel (62 VGPRs, no ring code); tiles
     // whose bytes exceed its 72 KiB stage are listed and hashed by the line-ring kernel
     // in a second launch on the same stream (none for BASELINE config 3).
@@ -761,7 +972,34 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
     const BucketParams none{};
     const BucketParams& p = bp ? *bp : none;
     const unsigned gl = g < 512u ? g : 512u;  // ring kernel: ~78 KiB LDS, two blocks per CU
-    if (e == hipSuccess) {
+    if (e == hipSuccess && (mode == kModeLean2Pin || mode == kModeLean2Step)) {
+      if (mode == kModeLean2Pin) {
+        if (h2) fnv_csr_lean2_kernel<true, false, 1><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+        else fnv_csr_lean2_kernel<false, false, 1><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      } else {
+        if (h2) fnv_csr_lean2_kernel<true, false, 2><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+        else fnv_csr_lean2_kernel<false, false, 2><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      }
+      if (h2) fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+      else fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      e = hipGetLastError();
+    } else if (e == hipSuccess && mode == kModeLean2Ring) {
+      if (bp) {
+        if (h2) fnv_csr_lean2_kernel<true, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, p);
+        else fnv_csr_lean2_kernel<false, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, p);
+      } else {
+        if (h2) fnv_csr_lean2_kernel<true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+        else fnv_csr_lean2_kernel<false><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      }
+      if (bp) {
+        if (h2) fnv_csr_ring_list_kernel<true, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, p);
+        else fnv_csr_ring_list_kernel<false, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, p);
+      } else {
+        if (h2) fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+        else fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      }
+      e = hipGetLastError();
+    } else if (e == hipSuccess) {
       if (bp) {
         if (h2) {
           fnv_csr_lean_kernel<true, 512, 4, 72, 1, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, p);

@@ -140,6 +140,68 @@ __device__ __forceinline__ void fnv_chunk16(uint32_t& lo, uint32_t& hi, uint4 c)
   }
 }
 
+// Same, with the zero half of the mad64 addend pair passed in and out (z == 0 is never
+// changed): kept in v50 across a loop of statements instead of re-materialised per chunk.
+template <int BANK = 0>
+__device__ __forceinline__ void fnv_chunk16z(uint32_t& lo, uint32_t& hi, uint4 c, uint32_t& z) {
+  if constexpr (BANK == 0) {
+    asm(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_P_PAIR("v42", "v43", "v[42:43]")
+        : "+{v48}"(lo), "+{v49}"(hi), "+{v50}"(z)
+        : "{v40}"(c.x), "{v41}"(c.y), "{v42}"(c.z), "{v43}"(c.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+        : K2H_P_CLOBBERS);
+  } else {
+    asm(K2H_P_PAIR("v44", "v45", "v[44:45]") K2H_P_PAIR("v46", "v47", "v[46:47]")
+        : "+{v48}"(lo), "+{v49}"(hi), "+{v50}"(z)
+        : "{v44}"(c.x), "{v45}"(c.y), "{v46}"(c.z), "{v47}"(c.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+        : K2H_P_CLOBBERS);
+  }
+}
+
+// A chunk loop whose chunk registers stay in the asm banks: step<BANK> hashes the chunk
+// held in bank BANK (v[40:43] or v[44:47]) while it issues the LDS read of the next
+// chunk into the other bank (`next`, a 32-bit LDS address).  The read is in the asm, so
+// the compiler neither waits for it nor copies it: the s_waitcnt lgkmcnt(1) inside waits
+// only for the read the previous step issued into this step's bank.
+template <int BANK>
+__device__ __forceinline__ void fnv_step_read(uint32_t& lo, uint32_t& hi, uint4& a, uint4& b, uint32_t next) {
+  if constexpr (BANK == 0) {
+    asm volatile("ds_read_b128 v[44:47], %[nx]\n\ts_waitcnt lgkmcnt(1)\n\t" K2H_P_PAIR("v40", "v41", "v[40:41]")
+                     K2H_P_PAIR("v42", "v43", "v[42:43]")
+                 : "+{v48}"(lo), "+{v49}"(hi), "+{v40}"(a.x), "+{v41}"(a.y), "+{v42}"(a.z), "+{v43}"(a.w),
+                   "+{v44}"(b.x), "+{v45}"(b.y), "+{v46}"(b.z), "+{v47}"(b.w)
+                 : [nx] "v"(next), "{v50}"(0u), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+                 : K2H_P_CLOBBERS);
+  } else {
+    asm volatile("ds_read_b128 v[40:43], %[nx]\n\ts_waitcnt lgkmcnt(1)\n\t" K2H_P_PAIR("v44", "v45", "v[44:45]")
+                     K2H_P_PAIR("v46", "v47", "v[46:47]")
+                 : "+{v48}"(lo), "+{v49}"(hi), "+{v40}"(a.x), "+{v41}"(a.y), "+{v42}"(a.z), "+{v43}"(a.w),
+                   "+{v44}"(b.x), "+{v45}"(b.y), "+{v46}"(b.z), "+{v47}"(b.w)
+                 : [nx] "v"(next), "{v50}"(0u), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+                 : K2H_P_CLOBBERS);
+  }
+}
+
+// Pin a chunk into bank 0 (before a step loop; waits for the value like any use).
+__device__ __forceinline__ void fnv_bank0_pin(uint4& a) {
+  asm volatile("" : "+{v40}"(a.x), "+{v41}"(a.y), "+{v42}"(a.z), "+{v43}"(a.w));
+}
+
+// After a step loop: the key's last chunk is in bank 0, or in bank 1 when `from1` (this
+// lane's loop ended on a bank-0 step); hash it as the last chunk (second-hash snapshot).
+__device__ __forceinline__ void fnv_step_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4& a,
+                                              uint4& b, bool from1) {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (from1)
+    asm volatile("v_mov_b32 v40, v44\n\tv_mov_b32 v41, v45\n\tv_mov_b32 v42, v46\n\tv_mov_b32 v43, v47"
+                 : "+{v40}"(a.x), "+{v41}"(a.y), "+{v42}"(a.z), "+{v43}"(a.w)
+                 : "{v44}"(b.x), "{v45}"(b.y), "{v46}"(b.z), "{v47}"(b.w));
+  asm volatile(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_X_PAIR_LAST("v42", "v43", "v[42:43]")
+               : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2), "+{v40}"(a.x), "+{v41}"(a.y),
+                 "+{v42}"(a.z), "+{v43}"(a.w)
+               : "{v50}"(0u), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+               : K2H_P_CLOBBERS);
+}
+
 // 32 bytes (two chunks), one statement.
 __device__ __forceinline__ void fnv_chunk32(uint32_t& lo, uint32_t& hi, uint4 a, uint4 b) {
   asm(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_P_PAIR("v42", "v43", "v[42:43]")
@@ -157,6 +219,14 @@ __device__ __forceinline__ void fnv_chunk16_last(uint32_t& lo, uint32_t& hi, uin
       : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2)
       : "{v40}"(c.x), "{v41}"(c.y), "{v42}"(c.z), "{v43}"(c.w), "{v50}"(0u), [p] "s"(kPrimeLo),
         [sel] "s"(kSmearSel)
+      : K2H_P_CLOBBERS);
+}
+
+__device__ __forceinline__ void fnv_chunk16_lastz(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2, uint4 c,
+                                                  uint32_t& z) {
+  asm(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_X_PAIR_LAST("v42", "v43", "v[42:43]")
+      : "+{v48}"(lo), "+{v49}"(hi), "={v60}"(lo2), "={v61}"(hi2), "+{v50}"(z)
+      : "{v40}"(c.x), "{v41}"(c.y), "{v42}"(c.z), "{v43}"(c.w), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
       : K2H_P_CLOBBERS);
 }
 

@@ -60,10 +60,14 @@ enum {
   kVariantLongProbeMem4 = 44,
   kVariantLongProbeMem256 = 45,
   kVariantLongProbeMemHalf4 = 46,
-  kVariantLongLines256 = 47,
+  kVariantLongLines256 = 47,      // fixed long keys (len % 256 == 0): 2 rounds of 256 B per lane (32 KiB)
   kVariantCsrTile = 48,           // csr: the round-1 default (512-key tile kernel with the ring inside)
   kVariantRalleGroup16 = 49,      // ralledata: 16 lanes per record (default 8), overlapped 16-byte tails
-  kVariantRalleByteTail = 50,     // ralledata: the round-1 assembly (16 lanes, tails one byte per lane)      // fixed long keys (len % 256 == 0): 2 rounds of 256 B per lane (32 KiB)
+  kVariantRalleByteTail = 50,     // ralledata: the round-1 assembly (16 lanes, tails one byte per lane)
+  kVariantCsrLeanRing = 51,       // csr: lean 512-key tiles + ring list, before the VALU trims (default: lean2)
+  kVariantCsrLean2Pin = 52,       // csr: lean2 with the chunk registers pinned to the asm banks (the pin
+                                  // forces an lgkmcnt(0) per chunk read: 6 % slower)
+  kVariantCsrLean2Step = 53,      // csr: lean2 with the asm step walker (reads inside the hash asm, no copies)
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with

@@ -651,7 +651,10 @@ hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, ui
                          : variant == kVariantCsrLean512x4 ? 8
                          : variant == kVariantCsrAlignProbe ? 9
                          : variant == kVariantCsrTile   ? 0
-                                                        : 10,
+                         : variant == kVariantCsrLeanRing ? 10
+                         : variant == kVariantCsrLean2Pin ? 12
+                         : variant == kVariantCsrLean2Step ? 13
+                                                        : 11,
                          stream, epi ? bp : nullptr);
 }
 

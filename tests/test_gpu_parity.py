@@ -17,7 +17,7 @@ from k2hash_amd import batch
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12, 16, 17, 18, 23, 24, 25, 26, 27, 29, 30, 31]
-CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21, 48]
+CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21, 48, 51, 52, 53]
 
 
 def dev_u8(torch, arr, device, pad_front=0):
