@@ -325,7 +325,7 @@ __device__ __forceinline__ uint32_t len_bin(uint64_t len) {
 enum {
   kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
   kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10,
-  kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13
+  kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13, kModeLean2Group = 14
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -711,6 +711,85 @@ __device__ __forceinline__ void lds_hash32s(bool valid, uint32_t rs, uint32_t re
   r2 = len == 1 ? r1 : pack2(lo2, hi2);
 }
 
+// The reference's second hash from the first and the key's last byte: h1 = (h2 ^
+// sext(b)) * P (lib/k2hashfunc.cc:53-56), P odd, so h2 = (h1 * P^-1) ^ sext(b); for a
+// one-byte key h2 = h1 (lib/k2hashfunc.cc:83), for an empty one 0.
+constexpr uint64_t prime_inverse() {
+  uint64_t x = 1099511628211ULL;
+  for (int i = 0; i < 6; ++i) x *= 2 - 1099511628211ULL * x;
+  return x;
+}
+static_assert(prime_inverse() * 1099511628211ULL == 1, "P^-1 mod 2^64");
+__device__ __forceinline__ uint64_t second_from_first(uint64_t h1v, uint32_t len, const uint8_t* key_end) {
+  if (len <= 1) return h1v;  // 0 for an empty key, h1 for a one-byte key
+  const int64_t sb = (int64_t)(int8_t)key_end[-1];
+  return (h1v * prime_inverse()) ^ (uint64_t)sb;
+}
+
+// Two keys per lane, back to back: key 0 (k0 >= 1 chunks unless the lane is idle) then
+// key 1 (k1 chunks, 0 = none), end-aligned chunks read from LDS, the switch to key 1
+// (save key 0's state, restart from key 1's S_p with its masked chunk 0) in a branch
+// that only the lanes switching at that step take.  Returns the two h1 values.
+__device__ __forceinline__ void pair_walk(uint32_t k0, uint32_t p0, const uint8_t* cp0, uint32_t k1, uint32_t p1,
+                                          const uint8_t* cp1, const uint64_t* spad, const uint4* masks,
+                                          uint64_t& h0, uint64_t& h1v) {
+  const uint32_t T = k0 + k1, sw = k0;
+  uint64_t st = spad[p0];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32);
+  const uint8_t* cp = cp0;
+  uint4 m = masks[p0];
+  uint4 c0 = ld16(cp0);
+  c0 = make_uint4(c0.x & m.x, c0.y & m.y, c0.z & m.z, c0.w & m.w);
+  uint4 c1 = c0;
+  uint64_t saved = 0;
+  bool odd = false;
+  if (T > 1) {
+    uint32_t t = 0;
+    for (;;) {
+      c1 = ld16(cp + 16u * (t + 1));
+      fnv_chunk16<0>(lo, hi, c0);
+      ++t;
+      if (t == sw) {
+        saved = pack2(lo, hi);
+        st = spad[p1];
+        lo = (uint32_t)st;
+        hi = (uint32_t)(st >> 32);
+        cp = cp1 - 16 * (int32_t)t;
+        m = masks[p1];
+        c1 = ld16(cp1);
+        c1 = make_uint4(c1.x & m.x, c1.y & m.y, c1.z & m.z, c1.w & m.w);
+      }
+      if (t + 1 >= T) {
+        odd = true;
+        break;
+      }
+      c0 = ld16(cp + 16u * (t + 1));
+      fnv_chunk16<1>(lo, hi, c1);
+      ++t;
+      if (t == sw) {
+        saved = pack2(lo, hi);
+        st = spad[p1];
+        lo = (uint32_t)st;
+        hi = (uint32_t)(st >> 32);
+        cp = cp1 - 16 * (int32_t)t;
+        m = masks[p1];
+        c0 = ld16(cp1);
+        c0 = make_uint4(c0.x & m.x, c0.y & m.y, c0.z & m.z, c0.w & m.w);
+      }
+      if (t + 1 >= T) break;
+    }
+  }
+  if (odd) c0 = c1;
+  fnv_chunk16<0>(lo, hi, c0);  // the last chunk of the lane's last key
+  if (k1) {
+    h0 = saved;
+    h1v = pack2(lo, hi);
+  } else {
+    h0 = pack2(lo, hi);
+    h1v = 0;
+  }
+}
+
 template <bool H2, bool EPI = false, int WALK = 0>
 __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
@@ -799,6 +878,37 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
   __syncthreads();                                   // ... and every other wave's
 
   const uint8_t* key0 = s_stage + 16 + delta;
+  if constexpr (WALK == 3) {
+    // Pair walk: lane i (0..255) takes sorted keys i and cnt-1-i, a short and a long one,
+    // and hashes them back to back; sums of the pair lengths are nearly equal across a
+    // wave, so the wave's length waste drops from 10.8 % (groups of 64 equal-class keys)
+    // to ~3.4 % on BASELINE config 3.
+    const uint32_t i = wave * 64u + lane;
+    const bool has_a = i < (cnt + 1u) / 2u, has_b = i < cnt / 2u;
+    const uint32_t ka = s_order[has_a ? i : 0u], kbi = s_order[has_b ? cnt - 1u - i : 0u];
+    const uint32_t ra = s_rel[ka], rae = s_rel[ka + 1], rb = s_rel[kbi], rbe = s_rel[kbi + 1];
+    const uint32_t la = has_a ? rae - ra : 0u, lb = has_b ? rbe - rb : 0u;
+    const uint32_t kA = (la + 15u) >> 4, kB = (lb + 15u) >> 4;
+    const uint32_t pA = (0u - la) & 15u, pB = (0u - lb) & 15u;
+    const uint8_t* cpA = key0 + (int32_t)(rae - 16u * kA);
+    const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
+    const bool only_b = kA == 0;  // key A empty (or absent): walk B alone
+    uint64_t hw0, hw1;
+    pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
+              hw0, hw1);
+    const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
+    if (has_a) {
+      h1[t0 + ka] = hA;
+      if constexpr (H2) h2[t0 + ka] = second_from_first(hA, la, key0 + rae);
+      if constexpr (EPI) bucket_emit<false>(bp, t0 + ka, hA);
+    }
+    if (has_b) {
+      h1[t0 + kbi] = hB;
+      if constexpr (H2) h2[t0 + kbi] = second_from_first(hB, lb, key0 + rbe);
+      if constexpr (EPI) bucket_emit<false>(bp, t0 + kbi, hB);
+    }
+    return;
+  }
   const uint32_t ngroups = (cnt + 63u) >> 6;
   const uint32_t wr = (wave + blockIdx.x) % NW;
   for (uint32_t it = 0; it * NW < ngroups; ++it) {
@@ -956,12 +1066,38 @@ SpadTable make_spad(uint64_t seed) {
   return t;
 }
 
+// lean2 tile kernel (walk WALK) + the ring pass over its oversize-tile list.
+template <int WALK>
+static hipError_t launch_lean2(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
+                               uint64_t* h2, uint32_t* scratch, unsigned g, unsigned gl, const BucketParams* bp,
+                               hipStream_t stream) {
+  if (bp) {
+    if (h2) {
+      fnv_csr_lean2_kernel<true, true, WALK><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, *bp);
+      fnv_csr_ring_list_kernel<true, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, *bp);
+    } else {
+      fnv_csr_lean2_kernel<false, true, WALK><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, *bp);
+      fnv_csr_ring_list_kernel<false, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, *bp);
+    }
+  } else {
+    if (h2) {
+      fnv_csr_lean2_kernel<true, false, WALK><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+      fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+    } else {
+      fnv_csr_lean2_kernel<false, false, WALK><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+    }
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
   SpadTable t = make_spad(seed);
   unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
   const uint8_t* b = (const uint8_t*)bytes;
-  if (mode == kModeLeanRing || mode == kModeLean2Ring || mode == kModeLean2Pin || mode == kModeLean2Step) {
+  if (mode == kModeLeanRing || mode == kModeLean2Ring || mode == kModeLean2Pin || mode == kModeLean2Step ||
+      mode == kModeLean2Group) {
     // Default: 512-key tiles staged by the lean kernel (62 VGPRs, no ring code); tiles
     // whose bytes exceed its 72 KiB stage are listed and hashed by the line-ring kernel
     // in a second launch on the same stream (none for BASELINE config 3).
@@ -972,33 +1108,11 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
     const BucketParams none{};
     const BucketParams& p = bp ? *bp : none;
     const unsigned gl = g < 512u ? g : 512u;  // ring kernel: ~78 KiB LDS, two blocks per CU
-    if (e == hipSuccess && (mode == kModeLean2Pin || mode == kModeLean2Step)) {
-      if (mode == kModeLean2Pin) {
-        if (h2) fnv_csr_lean2_kernel<true, false, 1><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
-        else fnv_csr_lean2_kernel<false, false, 1><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
-      } else {
-        if (h2) fnv_csr_lean2_kernel<true, false, 2><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
-        else fnv_csr_lean2_kernel<false, false, 2><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
-      }
-      if (h2) fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
-      else fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
-      e = hipGetLastError();
-    } else if (e == hipSuccess && mode == kModeLean2Ring) {
-      if (bp) {
-        if (h2) fnv_csr_lean2_kernel<true, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, p);
-        else fnv_csr_lean2_kernel<false, true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, p);
-      } else {
-        if (h2) fnv_csr_lean2_kernel<true><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
-        else fnv_csr_lean2_kernel<false><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
-      }
-      if (bp) {
-        if (h2) fnv_csr_ring_list_kernel<true, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, p);
-        else fnv_csr_ring_list_kernel<false, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, p);
-      } else {
-        if (h2) fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
-        else fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
-      }
-      e = hipGetLastError();
+    if (e == hipSuccess && mode != kModeLeanRing) {
+      e = mode == kModeLean2Pin    ? launch_lean2<1>(b, offsets, n, t, h1, h2, scratch, g, gl, bp, stream)
+          : mode == kModeLean2Step ? launch_lean2<2>(b, offsets, n, t, h1, h2, scratch, g, gl, bp, stream)
+          : mode == kModeLean2Group ? launch_lean2<0>(b, offsets, n, t, h1, h2, scratch, g, gl, bp, stream)
+                                    : launch_lean2<3>(b, offsets, n, t, h1, h2, scratch, g, gl, bp, stream);
     } else if (e == hipSuccess) {
       if (bp) {
         if (h2) {

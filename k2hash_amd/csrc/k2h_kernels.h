@@ -65,9 +65,11 @@ enum {
   kVariantRalleGroup16 = 49,      // ralledata: 16 lanes per record (default 8), overlapped 16-byte tails
   kVariantRalleByteTail = 50,     // ralledata: the round-1 assembly (16 lanes, tails one byte per lane)
   kVariantCsrLeanRing = 51,       // csr: lean 512-key tiles + ring list, before the VALU trims (default: lean2)
-  kVariantCsrLean2Pin = 52,       // csr: lean2 with the chunk registers pinned to the asm banks (the pin
+  kVariantCsrLean2Pin = 52,       // csr: lean2 group walk with the chunk registers pinned to the asm banks (the pin
                                   // forces an lgkmcnt(0) per chunk read: 6 % slower)
-  kVariantCsrLean2Step = 53,      // csr: lean2 with the asm step walker (reads inside the hash asm, no copies)
+  kVariantCsrLean2Step = 53,      // csr: lean2 group walk with the asm step walker (reads inside the hash asm, no copies)
+  kVariantCsrLean2Group = 54,     // csr: lean2 with one key per lane in groups of 64 (default: two keys per lane,
+                                  // short + long sorted partners, h2 from h1)
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with

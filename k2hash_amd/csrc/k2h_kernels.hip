@@ -654,6 +654,7 @@ hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, ui
                          : variant == kVariantCsrLeanRing ? 10
                          : variant == kVariantCsrLean2Pin ? 12
                          : variant == kVariantCsrLean2Step ? 13
+                         : variant == kVariantCsrLean2Group ? 14
                                                         : 11,
                          stream, epi ? bp : nullptr);
 }

@@ -115,7 +115,7 @@ def test_fused_fixed_vs_oracle(cuda, oracle, key_len, variant):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 3, 11, 19])
+@pytest.mark.parametrize("variant", [0, 3, 11, 19, 54])
 def test_fused_csr_vs_oracle(cuda, oracle, variant):
     import torch
     batch.set_variant(variant)

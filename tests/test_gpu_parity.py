@@ -17,7 +17,7 @@ from k2hash_amd import batch
 pytestmark = pytest.mark.gpu
 
 VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12, 16, 17, 18, 23, 24, 25, 26, 27, 29, 30, 31]
-CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21, 48, 51, 52, 53]
+CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21, 48, 51, 52, 53, 54]
 
 
 def dev_u8(torch, arr, device, pad_front=0):
@@ -218,7 +218,7 @@ def test_full_size_fixed_digest(cuda, oracle, digests, name):
     assert torch.equal(g1, h1)
 
 
-@pytest.mark.parametrize("variant", [0, 19, 20, 21, 48])
+@pytest.mark.parametrize("variant", [0, 19, 20, 21, 48, 54])
 @pytest.mark.parametrize("name", ["csr_8_256_64M", "csr_8_256_64K"])
 def test_full_size_csr_digest(cuda, oracle, digests, name, variant):
     import torch
