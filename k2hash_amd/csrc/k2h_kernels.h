@@ -70,6 +70,10 @@ enum {
   kVariantCsrLean2Step = 53,      // csr: lean2 group walk with the asm step walker (reads inside the hash asm, no copies)
   kVariantCsrLean2Group = 54,     // csr: lean2 with one key per lane in groups of 64 (default: two keys per lane,
                                   // short + long sorted partners, h2 from h1)
+  kVariantRalleProbeAligned = 55, // ralledata timing probes (WRONG blobs): aligned segment stores / header only
+  kVariantRalleProbeHeader = 56,
+  kVariantRalleBatch4 = 57,       // ralledata: 4 / 2 records per 8-lane group, loads batched (slower, A/B)
+  kVariantRalleBatch2 = 58,
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with

@@ -77,9 +77,10 @@ __global__ __launch_bounds__(256) void ralledata_assemble_kernel(RalleInputs in,
 // the two stores does not matter); only segments shorter than 16 bytes are copied byte
 // by byte.  G = 8 keeps most lanes busy on BASELINE-like records (keys 8-64 B, values
 // 0-256 B); G = 16 and the round-1 byte-tail form are A/B variants.
-template <int G, bool BYTE_TAIL = false>
+template <int G, bool BYTE_TAIL = false, int PROBE = 0>
 __device__ __forceinline__ void group_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len,
                                            uint32_t q) {
+  if constexpr (PROBE == 1) dst = (uint8_t*)((uintptr_t)dst & ~(uintptr_t)15);  // timing probe: aligned stores
   uint64_t full = len & ~15ull;
   for (uint64_t j = 16ull * q; j < full; j += 16ull * G)
     *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
@@ -92,7 +93,8 @@ __device__ __forceinline__ void group_copy(uint8_t* __restrict__ dst, const uint
   for (uint64_t t = full + q; t < len; t += G) dst[t] = src[t];  // the <= 15 tail bytes
 }
 
-template <int G, bool BYTE_TAIL = false>
+// PROBE (timing only, wrong blobs): 1 = segment stores 16-byte aligned, 2 = no segment copies.
+template <int G, bool BYTE_TAIL = false, int PROBE = 0>
 __global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
                                                               uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
   static_assert(G >= 5 && 64 % G == 0, "five lanes write the header");
@@ -115,14 +117,124 @@ __global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, ui
     *reinterpret_cast<u32x4_ua*>(b + 16 * q) =
         u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
   }
-  if (kl) group_copy<G, BYTE_TAIL>(b + 80, in.keys + in.koff[i], kl, q);
-  if (vl) group_copy<G, BYTE_TAIL>(b + 80 + kl, in.vals + in.voff[i], vl, q);
-  if (sl) group_copy<G, BYTE_TAIL>(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
-  if (al) group_copy<G, BYTE_TAIL>(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
+  if constexpr (PROBE != 2) {
+    if (kl) group_copy<G, BYTE_TAIL, PROBE>(b + 80, in.keys + in.koff[i], kl, q);
+    if (vl) group_copy<G, BYTE_TAIL, PROBE>(b + 80 + kl, in.vals + in.voff[i], vl, q);
+    if (sl) group_copy<G, BYTE_TAIL, PROBE>(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
+    if (al) group_copy<G, BYTE_TAIL, PROBE>(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
+  }
   if (blob_off && q == 0) {
     blob_off[i] = o;
     if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
   }
+}
+
+// Batched form (A/B variants 57-58, measured slower: 1.56 ms at 2 and 2.13 ms at 4 records
+// per group vs 1.50 for the group form -- the register cost (82 / 152 VGPRs) outweighs the
+// extra loads in flight).  Motivation: a header-only probe of the group form already
+// takes 0.62 of its 1.43 ms, so its waves look latency bound.  Here a
+// group of G lanes takes RPG consecutive records: all their offsets are loaded
+// together, and each segment is copied for all RPG records with straight-line,
+// predicated code (pieces 16q and 16q + 16G, the overlapped tail, short segments byte by
+// byte), so the loads of every record are in flight before the first store.  Pieces
+// beyond 32G bytes of a segment take a loop.
+template <int G, int RPG>
+__global__ __launch_bounds__(256) void ralledata_batch_kernel(RalleInputs in, uint64_t n,
+                                                              const uint64_t* __restrict__ h,
+                                                              uint8_t* __restrict__ out,
+                                                              uint64_t* __restrict__ blob_off) {
+  static_assert(G >= 8 && 64 % G == 0, "five lanes write the header, eight cover a short segment");
+  const uint64_t grp = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / G;
+  const uint32_t q = threadIdx.x % G;
+  if (grp * RPG >= n) return;
+  const uint64_t* offs[4] = {in.koff, in.voff, in.soff, in.aoff};
+  const uint8_t* bases[4] = {in.keys, in.vals, in.skeys, in.attrs};
+  uint64_t o0[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) o0[s] = offs[s] ? offs[s][0] : 0;
+
+  bool ok[RPG];
+  uint64_t rec[RPG], o[RPG];
+  uint32_t len[RPG][4];
+  uint64_t src[RPG][4];
+#pragma unroll
+  for (int r = 0; r < RPG; ++r) {
+    rec[r] = grp * RPG + r;
+    ok[r] = rec[r] < n;
+    const uint64_t i = ok[r] ? rec[r] : n - 1;
+    uint64_t ob = 80ull * i;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      uint64_t b = offs[s] ? offs[s][i] : 0, e = offs[s] ? offs[s][i + 1] : 0;
+      len[r][s] = (uint32_t)(e - b);
+      src[r][s] = (uint64_t)(uintptr_t)bases[s] + b;
+      ob += b - o0[s];
+    }
+    o[r] = ob;
+  }
+  // headers + blob offsets
+#pragma unroll
+  for (int r = 0; r < RPG; ++r) {
+    if (!ok[r]) continue;
+    uint8_t* b = out + o[r];
+    const uint64_t kl = len[r][0], vl = len[r][1], sl = len[r][2], al = len[r][3];
+    if (q < 5) {
+      uint64_t f0, f1;
+      switch (q) {
+        case 0: f0 = h[rec[r]]; f1 = h[n + rec[r]]; break;
+        case 1: f0 = kl; f1 = vl; break;
+        case 2: f0 = sl; f1 = al; break;
+        case 3: f0 = 80; f1 = 80 + kl; break;
+        default: f0 = 80 + kl + vl; f1 = 80 + kl + vl + sl; break;
+      }
+      *reinterpret_cast<u32x4_ua*>(b + 16 * q) =
+          u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
+    }
+    if (blob_off && q == 0) {
+      blob_off[rec[r]] = o[r];
+      if (rec[r] + 1 == n) blob_off[n] = o[r] + 80 + kl + vl + sl + al;
+    }
+  }
+  // segments, one after the other (a compiler barrier between them keeps the loads of
+  // one segment for all RPG records together without hoisting every segment's loads)
+  auto segment = [&](const int s) {
+    u32x4_ua pa[RPG], pb[RPG], pt[RPG];
+    uint8_t c0[RPG], c1[RPG];
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) {  // loads
+      const uint32_t L = ok[r] ? len[r][s] : 0u, full = L & ~15u;
+      const uint8_t* sp = (const uint8_t*)(uintptr_t)src[r][s];
+      if (16u * q < full) pa[r] = *reinterpret_cast<const u32x4_ua*>(sp + 16u * q);
+      if (16u * (q + G) < full) pb[r] = *reinterpret_cast<const u32x4_ua*>(sp + 16u * (q + G));
+      if (L >= 16u && (L & 15u) && q == G - 1) pt[r] = *reinterpret_cast<const u32x4_ua*>(sp + L - 16u);
+      if (L < 16u) {
+        if (q < L) c0[r] = sp[q];
+        if (q + G < L) c1[r] = sp[q + G];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < RPG; ++r) {  // stores
+      const uint32_t L = ok[r] ? len[r][s] : 0u, full = L & ~15u;
+      uint32_t before = 80u;
+      for (int t = 0; t < s; ++t) before += len[r][t];
+      uint8_t* dp = out + o[r] + before;
+      if (16u * q < full) *reinterpret_cast<u32x4_ua*>(dp + 16u * q) = pa[r];
+      if (16u * (q + G) < full) *reinterpret_cast<u32x4_ua*>(dp + 16u * (q + G)) = pb[r];
+      if (L >= 16u && (L & 15u) && q == G - 1) *reinterpret_cast<u32x4_ua*>(dp + L - 16u) = pt[r];
+      if (L < 16u) {
+        if (q < L) dp[q] = c0[r];
+        if (q + G < L) dp[q + G] = c1[r];
+      }
+      const uint8_t* sp = (const uint8_t*)(uintptr_t)src[r][s];
+      for (uint32_t j = 16u * (q + 2 * G); j < full; j += 16u * G)  // long segments
+        *reinterpret_cast<u32x4_ua*>(dp + j) = *reinterpret_cast<const u32x4_ua*>(sp + j);
+    }
+    asm volatile("" ::: "memory");
+  };
+  if (in.koff) segment(0);
+  if (in.voff) segment(1);
+  if (in.soff) segment(2);
+  if (in.aoff) segment(3);
 }
 
 }  // namespace
@@ -140,10 +252,18 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
   if (e == hipSuccess) {
     if (variant == kVariantRalleThread)
       ralledata_assemble_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else if (variant == kVariantRalleProbeAligned)
+      ralledata_group_kernel<8, false, 1><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else if (variant == kVariantRalleProbeHeader)
+      ralledata_group_kernel<8, false, 2><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     else if (variant == kVariantRalleGroup16)
       ralledata_group_kernel<16><<<(unsigned)((n * 16 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     else if (variant == kVariantRalleByteTail)
       ralledata_group_kernel<16, true><<<(unsigned)((n * 16 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else if (variant == kVariantRalleBatch4)
+      ralledata_batch_kernel<8, 4><<<(unsigned)(((n + 3) / 4 * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else if (variant == kVariantRalleBatch2)
+      ralledata_batch_kernel<8, 2><<<(unsigned)(((n + 1) / 2 * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     else
       ralledata_group_kernel<8><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     e = hipGetLastError();

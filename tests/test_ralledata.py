@@ -86,7 +86,7 @@ def test_host_matches_reference_fixture(cuda, golden):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 28, 49, 50])
+@pytest.mark.parametrize("variant", [0, 28, 49, 50, 57, 58])
 @pytest.mark.parametrize("segments", ["kv", "k", "kvsa", "ka"])
 def test_device_vs_oracle_random(cuda, oracle, segments, variant):
     import torch
