@@ -74,6 +74,8 @@ enum {
   kVariantRalleProbeHeader = 56,
   kVariantRalleBatch4 = 57,       // ralledata: 4 / 2 records per 8-lane group, loads batched (slower, A/B)
   kVariantRalleBatch2 = 58,
+  kVariantFixed32Pipe64 = 59,     // fixed32: persistent, next tile's loads issued before hashing the current
+  kVariantFixed32Pipe256 = 60,    // (one-wave / 256-thread blocks, two keys per lane)
 };
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with

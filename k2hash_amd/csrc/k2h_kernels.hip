@@ -292,6 +292,75 @@ __global__ __launch_bounds__(BS) void fnv_fixed32_kpt_kernel(const uint4* __rest
 }
 
 // ---------------------------------------------------------------------------
+// fixed32, software-pipelined persistent blocks: each block walks tiles of 2*BS keys
+// (two keys per lane) with a grid stride, and the loads of its next tile are issued
+// before it hashes the current one, so every wave always has 4 KiB in flight (the flat
+// kernel has loads in flight only while it waits).  Loads are unconditional (past the
+// last tile a block re-reads its current one), so the compiler's vmcnt waits are exact.
+// ---------------------------------------------------------------------------
+template <bool H2, int BS>
+__global__ __launch_bounds__(BS) void fnv_fixed32_pipe_kernel(const uint4* __restrict__ keys, uint64_t n,
+                                                              uint64_t seed, uint64_t* __restrict__ h1,
+                                                              uint64_t* __restrict__ h2) {
+  const uint64_t ntiles = (n + 2 * BS - 1) / (2 * BS);
+  const uint64_t stride = gridDim.x;
+  uint64_t t = blockIdx.x;
+  if (t >= ntiles) return;
+  auto load = [&](uint64_t tile, uint4(&v)[4]) {
+    const uint64_t i0 = tile * (2 * BS) + threadIdx.x, i1 = i0 + BS;
+    const uint64_t a = i0 < n ? i0 : n - 1, b = i1 < n ? i1 : n - 1;
+    v[0] = ld_nt(keys + 2 * a);
+    v[1] = ld_nt(keys + 2 * a + 1);
+    v[2] = ld_nt(keys + 2 * b);
+    v[3] = ld_nt(keys + 2 * b + 1);
+  };
+  auto work = [&](uint64_t tile, const uint4(&v)[4]) {
+    const uint64_t i0 = tile * (2 * BS) + threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const uint64_t i = i0 + BS * j;
+      uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2, hi2;
+      if constexpr (H2) fnv_chunk32_last(lo, hi, lo2, hi2, v[2 * j], v[2 * j + 1]);
+      else fnv_chunk32(lo, hi, v[2 * j], v[2 * j + 1]);
+      if (i < n) {
+        st_nt(h1 + i, pack(lo, hi));
+        if constexpr (H2) st_nt(h2 + i, pack(lo2, hi2));
+      }
+    }
+  };
+  uint4 A[4], B[4];
+  load(t, A);
+  for (;;) {
+    const uint64_t t1 = t + stride;
+    load(t1 < ntiles ? t1 : t, B);
+    work(t, A);
+    if (t1 >= ntiles) break;
+    const uint64_t t2 = t1 + stride;
+    load(t2 < ntiles ? t2 : t1, A);
+    work(t1, B);
+    if (t2 >= ntiles) break;
+    t = t2;
+  }
+}
+
+template <bool H2, int BS>
+static unsigned pipe_grid(uint64_t ntiles) {
+  static int per_cu = 0, cus = 0;
+  if (!per_cu) {
+    int dev = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)fnv_fixed32_pipe_kernel<H2, BS>, BS, 0) !=
+            hipSuccess ||
+        per_cu <= 0)
+      per_cu = 2048 / BS;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const uint64_t g = (uint64_t)cus * (uint64_t)per_cu;
+  return (unsigned)(ntiles < g ? ntiles : g);
+}
+
+// ---------------------------------------------------------------------------
 // fixed32, LDS-DMA ring: one-wave blocks, persistent.  Wave w hashes tiles of 64 keys
 // (2 KiB) w, w + W, w + 2W, ... and streams them through a private ring of S LDS slots
 // with global_load_lds_dwordx4 (two fully coalesced 1 KiB pieces per tile, no VGPRs
@@ -459,6 +528,18 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
         }
         if (h2) fnv_fixed32_kpt_kernel<true, 2, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_kpt_kernel<false, 2, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
+      case kVariantFixed32Pipe64: {
+        const uint64_t nt = (n + 127) / 128;
+        if (h2) fnv_fixed32_pipe_kernel<true, 64><<<pipe_grid<true, 64>(nt), 64, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_pipe_kernel<false, 64><<<pipe_grid<false, 64>(nt), 64, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
+      case kVariantFixed32Pipe256: {
+        const uint64_t nt = (n + 511) / 512;
+        if (h2) fnv_fixed32_pipe_kernel<true, 256><<<pipe_grid<true, 256>(nt), 256, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_pipe_kernel<false, 256><<<pipe_grid<false, 256>(nt), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
       }
       case kVariantFixed32Nt256:

@@ -16,7 +16,7 @@ from k2hash_amd import batch
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12, 16, 17, 18, 23, 24, 25, 26, 27, 29, 30, 31]
+VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12, 16, 17, 18, 23, 24, 25, 26, 27, 29, 30, 31, 59, 60]
 CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21, 48, 51, 52, 53, 54]
 
 
@@ -54,7 +54,7 @@ def test_fixed32_vs_oracle(cuda, oracle, n, variant):
     assert np.array_equal(host_u64(g1), r1)
 
 
-@pytest.mark.parametrize("variant", [0, 5, 6, 16, 17, 18])
+@pytest.mark.parametrize("variant", [0, 5, 6, 16, 17, 18, 59, 60])
 @pytest.mark.parametrize("n", [(1 << 21) + 17, 3 << 20])
 def test_fixed32_persistent_many_tiles(cuda, oracle, n, variant):
     """Persistent / ring kernels at sizes where every wave walks many tiles (the
