@@ -195,6 +195,27 @@ int k2h_amd_archive_prehash_host(const void* file, uint64_t size, const k2h_amd_
                                  uint64_t* h1, uint64_t* h2, uint64_t* new_h1, uint64_t* new_h2, uint32_t flags,
                                  int device);
 
+/* k2himport inputs (tests/k2himport.cc:74-117): k2h_amd_import_scan splits a TSV
+ * (key TAB value NEWLINE) or mdbm_export file (five header lines ending "HEADER=END",
+ * then key line / value line) into records exactly as the tool's std::getline loops
+ * do, and reports each key and value as the C string K2HShm::Set(const char*, const
+ * char*) stores (lib/k2hshm.cc:2081-2083): *_len = strlen, i.e. cut at a NUL byte.
+ * recs may be NULL to count only; a bad mdbm header returns K2H_AMD_EINVAL (the tool
+ * exits).  Faithful to getline: an mdbm key line ending at EOF reports the previous
+ * record's value range (the string a failed getline leaves untouched).  k2h_amd_import_prehash_host hashes every key as key + NUL on the GPU (the
+ * bytes Set hashes).  Host pointers. */
+#define K2H_AMD_IMPORT_TSV 0
+#define K2H_AMD_IMPORT_MDBM 1
+typedef struct k2h_amd_import_rec {
+  uint64_t key_off, key_len; /* absolute offset in the file, strlen of the key */
+  uint64_t val_off, val_len; /* likewise for the value */
+} k2h_amd_import_rec;
+
+int k2h_amd_import_scan(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
+                        uint64_t* count);
+int k2h_amd_import_prehash_host(const void* file, uint64_t size, const k2h_amd_import_rec* recs, uint64_t count,
+                                uint64_t* h1, uint64_t* h2, uint32_t flags, int device);
+
 /* Identity / diagnostics. */
 const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */
 const char* k2h_amd_strerror(int code); /* message for `code`, with the last HIP error if any */

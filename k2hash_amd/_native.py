@@ -21,6 +21,7 @@ K2H_AMD_ENOMEM = -3
 K2H_AMD_ENODEV = -4
 K2H_AMD_FLAG_STD_FNV = 0x1
 K2H_AMD_FLAG_CSTR = 0x2
+K2H_AMD_IMPORT_TSV, K2H_AMD_IMPORT_MDBM = 0, 1
 
 _u64 = ctypes.c_uint64
 _p = ctypes.c_void_p
@@ -44,6 +45,8 @@ SIGNATURES = {
     "k2h_amd_hash_ranges": (ctypes.c_int, [_p, _p, _p, _u64, _p, _p, ctypes.c_uint32, _p]),
     "k2h_amd_archive_scan": (ctypes.c_int, [_p, _u64, _p, _u64, _p]),
     "k2h_amd_archive_prehash_host": (ctypes.c_int, [_p, _u64, _p, _u64, _p, _p, _p, _p, ctypes.c_uint32, ctypes.c_int]),
+    "k2h_amd_import_scan": (ctypes.c_int, [_p, _u64, ctypes.c_int, _p, _u64, _p]),
+    "k2h_amd_import_prehash_host": (ctypes.c_int, [_p, _u64, _p, _u64, _p, _p, ctypes.c_uint32, ctypes.c_int]),
     "k2h_amd_version": (ctypes.c_char_p, []),
     "k2h_amd_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "k2h_amd_set_variant": (ctypes.c_int, [ctypes.c_int]),

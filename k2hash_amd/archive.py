@@ -78,3 +78,43 @@ def hash_ranges(base, starts, lens, second: bool = False, cstr: bool = False, st
                                                  _stream_handle(stream))
     _native.check(rc)
     return h1, h2
+
+
+# ---------------------------------------------------------------------------
+# k2himport inputs (tests/k2himport.cc:74-117): TSV and mdbm_export files.
+# ---------------------------------------------------------------------------
+IMPORT_TSV, IMPORT_MDBM = _native.K2H_AMD_IMPORT_TSV, _native.K2H_AMD_IMPORT_MDBM
+# struct k2h_amd_import_rec (include/k2hash_amd.h)
+IMPORT_DTYPE = np.dtype([("key_off", "<u8"), ("key_len", "<u8"), ("val_off", "<u8"), ("val_len", "<u8")])
+
+
+def import_scan(data, fmt: str = "tsv") -> np.ndarray:
+    """Records of a k2himport input, split exactly as the tool's getline loops do, each key
+    and value as the C string K2HShm::Set(const char*, const char*) stores (lengths are
+    strlen).  fmt: "tsv" or "mdbm"; a bad mdbm header raises (the tool exits)."""
+    f = _buf(data)
+    code = {"tsv": IMPORT_TSV, "mdbm": IMPORT_MDBM}[fmt]
+    ptr = ctypes.c_void_p(f.ctypes.data if f.size else 1)
+    lib = _native.batch_lib()
+    cnt = ctypes.c_uint64()
+    _native.check(lib.k2h_amd_import_scan(ptr, f.size, code, None, 0, ctypes.byref(cnt)))
+    recs = np.zeros(cnt.value, IMPORT_DTYPE)
+    _native.check(lib.k2h_amd_import_scan(ptr, f.size, code, ctypes.c_void_p(recs.ctypes.data if recs.size else 1),
+                                          recs.size, ctypes.byref(cnt)))
+    return recs
+
+
+def import_prehash(data, recs=None, fmt: str = "tsv", std_fnv: bool = False, device: int = 0):
+    """(h1, h2) of every record's key hashed as key + NUL on the GPU -- the bytes
+    K2HShm::Set(const char*) hashes (lib/k2hshm.cc:2081-2083)."""
+    f = _buf(data)
+    if recs is None:
+        recs = import_scan(f, fmt)
+    n = recs.size
+    h1, h2 = np.zeros(n, np.uint64), np.zeros(n, np.uint64)
+    if n:
+        _native.check(_native.batch_lib().k2h_amd_import_prehash_host(
+            ctypes.c_void_p(f.ctypes.data if f.size else 1), f.size, ctypes.c_void_p(recs.ctypes.data), n,
+            ctypes.c_void_p(h1.ctypes.data), ctypes.c_void_p(h2.ctypes.data), FLAG_STD_FNV if std_fnv else 0,
+            device))
+    return h1, h2
