@@ -216,6 +216,17 @@ int k2h_amd_import_scan(const void* file, uint64_t size, int format, k2h_amd_imp
 int k2h_amd_import_prehash_host(const void* file, uint64_t size, const k2h_amd_import_rec* recs, uint64_t count,
                                 uint64_t* h1, uint64_t* h2, uint32_t flags, int device);
 
+/* The same scan for a file already in device memory (file, recs: device pointers;
+ * count: host), with no host pass: record ends are the newlines of the lines that hold
+ * a TAB (TSV) or every second line after the header (mdbm), found by parallel passes
+ * (k2hash_amd/csrc/k2h_import_dev.hip).  Same records, same errors as
+ * k2h_amd_import_scan; synchronises `stream`.  k2h_amd_import_prehash hashes every
+ * record's key as key + NUL from the device-resident file (async on `stream`). */
+int k2h_amd_import_scan_device(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
+                               uint64_t* count, void* stream);
+int k2h_amd_import_prehash(const void* file, const k2h_amd_import_rec* recs, uint64_t n, uint64_t* h1, uint64_t* h2,
+                           uint32_t flags, void* stream);
+
 /* Identity / diagnostics. */
 const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */
 const char* k2h_amd_strerror(int code); /* message for `code`, with the last HIP error if any */

@@ -118,3 +118,39 @@ def import_prehash(data, recs=None, fmt: str = "tsv", std_fnv: bool = False, dev
             ctypes.c_void_p(h1.ctypes.data), ctypes.c_void_p(h2.ctypes.data), FLAG_STD_FNV if std_fnv else 0,
             device))
     return h1, h2
+
+
+def import_scan_device(file, fmt: str = "tsv", stream=None):
+    """import_scan for a file already in device memory (uint8 device tensor), with no
+    host pass (k2h_amd_import_scan_device).  Returns an (n, 4) int64 device tensor of
+    (key_off, key_len, val_off, val_len) rows -- struct k2h_amd_import_rec."""
+    torch = _torch()
+    _check_dev(file, "file", torch.uint8)
+    code = {"tsv": IMPORT_TSV, "mdbm": IMPORT_MDBM}[fmt]
+    lib = _native.batch_lib()
+    fp = ctypes.c_void_p(file.data_ptr() or 1)
+    cnt = ctypes.c_uint64()
+    _native.check(lib.k2h_amd_import_scan_device(fp, file.numel(), code, None, 0, ctypes.byref(cnt),
+                                                 _stream_handle(stream)))
+    recs = torch.empty((cnt.value, 4), dtype=torch.int64, device=file.device)
+    if cnt.value:
+        _native.check(lib.k2h_amd_import_scan_device(fp, file.numel(), code, _dev_ptr(recs), cnt.value,
+                                                     ctypes.byref(cnt), _stream_handle(stream)))
+    return recs
+
+
+def import_prehash_device(file, recs, std_fnv: bool = False, stream=None):
+    """(h1, h2) device tensors of every record's key hashed as key + NUL, from the
+    device-resident file and the records of import_scan_device."""
+    torch = _torch()
+    _check_dev(file, "file", torch.uint8)
+    _check_dev(recs, "recs", torch.int64)
+    if recs.dim() != 2 or recs.shape[1] != 4 or not recs.is_contiguous():
+        raise ValueError("recs must be a contiguous (n, 4) int64 tensor")
+    n = recs.shape[0]
+    h1 = torch.empty(n, dtype=torch.int64, device=file.device)
+    h2 = torch.empty(n, dtype=torch.int64, device=file.device)
+    _native.check(_native.batch_lib().k2h_amd_import_prehash(
+        ctypes.c_void_p(file.data_ptr() or 1), _dev_ptr(recs), n, _dev_ptr(h1), _dev_ptr(h2),
+        FLAG_STD_FNV if std_fnv else 0, _stream_handle(stream)))
+    return h1, h2

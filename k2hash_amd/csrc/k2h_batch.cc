@@ -416,6 +416,27 @@ __attribute__((visibility("default"))) int k2h_amd_hash_ranges(const void* base,
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_ranges", e);
 }
 
+// k2himport inputs in device memory (include/k2hash_amd.h section 5)
+__attribute__((visibility("default"))) int k2h_amd_import_scan_device(const void* file, uint64_t size, int format,
+                                                                      k2h_amd_import_rec* recs, uint64_t cap,
+                                                                      uint64_t* count, void* stream) {
+  if (!count || (size && !file) || (format != K2H_AMD_IMPORT_TSV && format != K2H_AMD_IMPORT_MDBM))
+    return fail(K2H_AMD_EINVAL, "import_scan_device: NULL count/file or bad format");
+  hipError_t e = hipSuccess;
+  int rc = k2h::launch_import_scan(file, size, format, recs, cap, count, (hipStream_t)stream, &e);
+  if (rc == K2H_AMD_EHIP) return fail(rc, "launch_import_scan", e);
+  return rc == K2H_AMD_OK ? rc : fail(rc, "import_scan_device: not a mdbm file, or more records than cap");
+}
+
+__attribute__((visibility("default"))) int k2h_amd_import_prehash(const void* file, const k2h_amd_import_rec* recs,
+                                                                  uint64_t n, uint64_t* h1, uint64_t* h2,
+                                                                  uint32_t flags, void* stream) {
+  if (n == 0) return K2H_AMD_OK;
+  if (!file || !recs || !h1) return fail(K2H_AMD_EINVAL, "import_prehash: NULL file/recs/h1");
+  hipError_t e = k2h::launch_import_prehash(file, recs, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_import_prehash", e);
+}
+
 // ---------------------------------------------------------------------------
 // RALLEDATA producer (include/k2hash_amd.h section 4)
 // ---------------------------------------------------------------------------

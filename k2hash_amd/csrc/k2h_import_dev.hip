@@ -1,0 +1,367 @@
+// k2hash_amd -- k2himport input scan on the GPU.
+//
+// The same records as the host scanner (k2h_import.cc, restating the std::getline loops
+// of tests/k2himport.cc:74-117) for a file that already sits in HBM, without a host pass:
+//
+// TSV (ConvertfromTsv, tests/k2himport.cc:74-89).  A record's key runs from the record
+// start to the first TAB (across newlines), its value from there to the next '\n'.  So a
+// record ends exactly at the newline of every line that holds a TAB, and the lines with
+// no TAB in front of it belong to its key.  Record ends are therefore a per-line
+// predicate and the loop needs no sequential walk: (1) newline positions by a per-chunk
+// count + scan + ordered write, (2) per line its first TAB and its first NUL (before and
+// after that TAB; keys and values are cut there, c_str()/strlen), (3) the TAB lines
+// compacted into records.  The bytes after the last newline form a last line whose
+// value ends at EOF; if it holds no TAB the key getline hits EOF and it is dropped,
+// as is a trailing run of newline-terminated lines with no TAB.
+// mdbm (ConvertfromMdbm, tests/k2himport.cc:95-117).  Five header lines (the fifth
+// "HEADER=END", checked on the host from the first newline positions), then line
+// pairs; the EOF rules of the host scanner (an empty value after a key line that ends
+// the file with '\n', the previous record's value after a key line that ends at EOF).
+//
+// Traffic: the file is read three times (count, positions, lines); outputs are 8 B per
+// line plus 32 B per record.  Every pass is a streaming read.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <stdint.h>
+#include <string.h>
+
+#include "../../include/k2hash_amd.h"
+#include "k2h_kernels.h"
+
+namespace k2h {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kBytesPerThread = 64;
+constexpr uint64_t kChunk = (uint64_t)kThreads * kBytesPerThread;  // 16 KiB per block
+constexpr uint64_t kNone = ~0ull;
+
+// Exact per-byte "equals c" mask of a 32-bit word: bit 7 of each matching byte.
+__device__ inline uint32_t eq_mask(uint32_t w, uint32_t c4) {
+  uint32_t v = w ^ c4;
+  uint32_t t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
+  return ~(t | v | 0x7F7F7F7Fu);
+}
+
+// Bytes [b, e) of this thread's 64-byte span, as 16 words with out-of-range bytes
+// replaced by a non-newline value; aligned fast path when the span is whole.
+__device__ inline void load_span(const uint8_t* f, uint64_t size, uint64_t b, uint32_t w[16]) {
+  if (b + 64 <= size && (((uintptr_t)(f + b)) & 15) == 0) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4* p = reinterpret_cast<const u32x4*>(f + b);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      u32x4 v = __builtin_nontemporal_load(p + q);
+      w[4 * q] = v.x, w[4 * q + 1] = v.y, w[4 * q + 2] = v.z, w[4 * q + 3] = v.w;
+    }
+    return;
+  }
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    uint32_t x = 0x01010101u;
+    for (int j = 0; j < 4; ++j) {
+      uint64_t i = b + 4 * k + j;
+      if (i < size) x = (x & ~(0xFFu << (8 * j))) | ((uint32_t)f[i] << (8 * j));
+    }
+    w[k] = x;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void nl_count_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                            uint64_t* __restrict__ block_cnt) {
+  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
+  uint32_t c = 0;
+  if (b < size) {
+    uint32_t w[16];
+    load_span(f, size, b, w);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c += __popc(eq_mask(w[k], 0x0A0A0A0Au));
+  }
+  typedef hipcub::BlockReduce<uint32_t, kThreads> Reduce;
+  __shared__ typename Reduce::TempStorage tmp;
+  uint32_t s = Reduce(tmp).Sum(c);
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = s;  // widened for the scan
+}
+
+// block_base = exclusive scan of block_cnt
+__global__ __launch_bounds__(kThreads) void nl_write_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                            const uint64_t* __restrict__ block_base,
+                                                            uint64_t* __restrict__ nl) {
+  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
+  uint32_t w[16];
+  uint32_t c = 0;
+  if (b < size) {
+    load_span(f, size, b, w);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      w[k] = eq_mask(w[k], 0x0A0A0A0Au);
+      c += __popc(w[k]);
+    }
+  }
+  typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  uint32_t o;
+  Scan(tmp).ExclusiveSum(c, o);
+  if (!c) return;
+  uint64_t* out = nl + block_base[blockIdx.x] + o;
+  for (int k = 0; k < 16; ++k) {
+    uint32_t m = w[k];
+    while (m) {
+      int bit = __builtin_ctz(m);
+      *out++ = b + 4 * k + (bit >> 3);
+      m &= m - 1;
+    }
+  }
+}
+
+struct LineInfo {
+  uint64_t tab;       // first TAB in the line, or kNone
+  uint64_t nul;       // first NUL in the line (anywhere), or kNone
+  uint64_t nul_tab;   // first NUL after the first TAB, or kNone
+};
+
+__device__ inline uint64_t line_begin(const uint64_t* nl, uint64_t j) { return j ? nl[j - 1] + 1 : 0; }
+__device__ inline uint64_t line_end(const uint64_t* nl, uint64_t nnl, uint64_t size, uint64_t j) {
+  return j < nnl ? nl[j] : size;
+}
+
+// One thread per line: its first TAB and first NUL before / after that TAB.
+__global__ __launch_bounds__(kThreads) void line_info_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                             const uint64_t* __restrict__ nl, uint64_t nnl,
+                                                             uint64_t nlines, LineInfo* __restrict__ info) {
+  const uint64_t j = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (j >= nlines) return;
+  const uint64_t lb = line_begin(nl, j), le = line_end(nl, nnl, size, j);
+  LineInfo r{kNone, kNone, kNone};
+  uint64_t i = lb;
+  // head bytes up to a 4-byte boundary, then words, then the tail
+  for (; i < le && ((uintptr_t)(f + i) & 3); ++i) {
+    uint8_t c = f[i];
+    if (c == 0) {
+      if (r.nul == kNone) r.nul = i;
+      if (r.tab != kNone && r.nul_tab == kNone) r.nul_tab = i;
+    } else if (c == 9 && r.tab == kNone) r.tab = i;
+  }
+  for (; i + 4 <= le; i += 4) {
+    const uint32_t w = *reinterpret_cast<const uint32_t*>(f + i);
+    uint32_t mz = eq_mask(w, 0), mt = eq_mask(w, 0x09090909u);
+    if (!(mz | mt)) continue;
+    for (int k = 0; k < 4; ++k) {
+      const uint32_t bit = 0x80u << (8 * k);
+      if (mz & bit) {
+        if (r.nul == kNone) r.nul = i + k;
+        if (r.tab != kNone && r.nul_tab == kNone) r.nul_tab = i + k;
+      } else if ((mt & bit) && r.tab == kNone) r.tab = i + k;
+    }
+    if (r.tab != kNone && r.nul_tab != kNone) {  // nothing more to learn
+      i = le;
+      break;
+    }
+  }
+  for (; i < le; ++i) {
+    uint8_t c = f[i];
+    if (c == 0) {
+      if (r.nul == kNone) r.nul = i;
+      if (r.tab != kNone && r.nul_tab == kNone) r.nul_tab = i;
+    } else if (c == 9 && r.tab == kNone) r.tab = i;
+  }
+  info[j] = r;
+}
+
+struct HasTab {
+  const LineInfo* info;
+  __host__ __device__ bool operator()(const uint64_t& j) const { return info[j].tab != kNone; }
+};
+
+// TSV: record r ends at TAB line rl[r]; its key starts after the previous TAB line.
+__global__ __launch_bounds__(kThreads) void tsv_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
+                                                               uint64_t size, const LineInfo* __restrict__ info,
+                                                               const uint64_t* __restrict__ rl, uint64_t nrec,
+                                                               k2h_amd_import_rec* __restrict__ recs) {
+  const uint64_t r = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (r >= nrec) return;
+  const uint64_t j1 = rl[r], j0 = r ? rl[r - 1] + 1 : 0;
+  const uint64_t kb = line_begin(nl, j0);
+  const LineInfo L = info[j1];
+  uint64_t kend = L.tab;
+  for (uint64_t j = j0; j < j1; ++j)  // key lines before the TAB line (usually none)
+    if (info[j].nul != kNone) {
+      kend = info[j].nul;
+      break;
+    }
+  if (kend == L.tab && L.nul != kNone && L.nul < L.tab) kend = L.nul;
+  const uint64_t vb = L.tab + 1, ve = L.nul_tab != kNone ? L.nul_tab : line_end(nl, nnl, size, j1);
+  k2h_amd_import_rec o;
+  o.key_off = kb;
+  o.key_len = kend - kb;
+  o.val_off = vb;
+  o.val_len = ve - vb;  // a TAB that ends the file: getline fails, empty value at EOF
+  recs[r] = o;
+}
+
+// mdbm: key line 5 + 2r, value line 6 + 2r (see the header comment for the EOF rules).
+__global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
+                                                                uint64_t size, const LineInfo* __restrict__ info,
+                                                                uint64_t nlines, uint64_t nrec, uint64_t body,
+                                                                k2h_amd_import_rec* __restrict__ recs) {
+  const uint64_t r = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (r >= nrec) return;
+  const uint64_t kl = 5 + 2 * r;
+  auto cut = [&](uint64_t j) {  // strlen of line j's C string
+    const uint64_t b = line_begin(nl, j), e = line_end(nl, nnl, size, j);
+    return (info[j].nul != kNone ? info[j].nul : e) - b;
+  };
+  k2h_amd_import_rec o;
+  o.key_off = line_begin(nl, kl);
+  o.key_len = cut(kl);
+  if (kl < nnl) {  // key line ends in '\n'
+    const uint64_t vl = kl + 1;
+    if (vl < nlines) {
+      o.val_off = line_begin(nl, vl);
+      o.val_len = cut(vl);
+    } else {  // the file ends after the key line: the value getline fails
+      o.val_off = size;
+      o.val_len = 0;
+    }
+  } else if (r) {  // key line at EOF: the previous record's value (getline kept it)
+    o.val_off = line_begin(nl, kl - 1);
+    o.val_len = cut(kl - 1);
+  } else {
+    o.val_off = body;
+    o.val_len = 0;
+  }
+  recs[r] = o;
+}
+
+__global__ __launch_bounds__(kThreads) void split_keys_kernel(const k2h_amd_import_rec* __restrict__ recs, uint64_t n,
+                                                              uint64_t* __restrict__ starts,
+                                                              uint64_t* __restrict__ lens) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  starts[i] = recs[i].key_off;
+  lens[i] = recs[i].key_len;
+}
+
+unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
+
+}  // namespace
+
+// Returns K2H_AMD_* codes (the HIP error, if any, in *herr).
+int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
+                       uint64_t* count, hipStream_t stream, hipError_t* herr) {
+  const uint8_t* f = (const uint8_t*)file;
+  *herr = hipSuccess;
+  *count = 0;
+  const uint64_t nblk = size ? (size + kChunk - 1) / kChunk : 0;
+  if (nblk > 0x7FFFFFFFull) return K2H_AMD_EINVAL;
+  uint64_t* bcnt = nullptr;
+  uint64_t *bbase = nullptr, *nl = nullptr, *rl = nullptr, *nsel = nullptr;
+  LineInfo* info = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  uint64_t nnl = 0, nlines = 0, nrec = 0, last_nl = 0;
+  int rc = K2H_AMD_OK;
+  hipError_t e = hipSuccess;
+#define K2H_TRY(x) \
+  do {             \
+    if (e == hipSuccess) e = (x); \
+  } while (0)
+  if (nblk) {
+    K2H_TRY(hipMallocAsync((void**)&bcnt, nblk * 8, stream));
+    K2H_TRY(hipMallocAsync((void**)&bbase, (nblk + 1) * 8, stream));
+    if (e == hipSuccess) {
+      nl_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt);
+      e = hipGetLastError();
+    }
+    K2H_TRY(hipMemsetAsync(bbase, 0, 8, stream));
+    K2H_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, bcnt, bbase + 1, nblk, stream));
+    K2H_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
+    K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, bcnt, bbase + 1, nblk, stream));
+    K2H_TRY(hipMemcpyAsync(&nnl, bbase + nblk, 8, hipMemcpyDeviceToHost, stream));
+    K2H_TRY(hipStreamSynchronize(stream));
+    K2H_TRY(hipMallocAsync((void**)&nl, (nnl ? nnl : 1) * 8, stream));
+    if (e == hipSuccess && nnl) {
+      nl_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, nl);
+      e = hipGetLastError();
+      K2H_TRY(hipMemcpyAsync(&last_nl, nl + nnl - 1, 8, hipMemcpyDeviceToHost, stream));
+      K2H_TRY(hipStreamSynchronize(stream));
+    }
+    // lines: one per newline, plus the bytes after the last newline if any
+    nlines = nnl + ((nnl ? last_nl + 1 : 0) < size ? 1 : 0);
+    K2H_TRY(hipMallocAsync((void**)&info, (nlines ? nlines : 1) * sizeof(LineInfo), stream));
+    if (e == hipSuccess && nlines) {
+      line_info_kernel<<<blocks_for(nlines), kThreads, 0, stream>>>(f, size, nl, nnl, nlines, info);
+      e = hipGetLastError();
+    }
+  }
+  if (e == hipSuccess && format == K2H_AMD_IMPORT_TSV && nlines) {
+    if (tmp) (void)hipFreeAsync(tmp, stream);
+    tmp = nullptr;
+    tmp_bytes = 0;
+    K2H_TRY(hipMallocAsync((void**)&rl, nlines * 8, stream));
+    K2H_TRY(hipMallocAsync((void**)&nsel, 8, stream));
+    hipcub::CountingInputIterator<uint64_t> it(0);
+    K2H_TRY(hipcub::DeviceSelect::If(nullptr, tmp_bytes, it, rl, nsel, nlines, HasTab{info}, stream));
+    K2H_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
+    K2H_TRY(hipcub::DeviceSelect::If(tmp, tmp_bytes, it, rl, nsel, nlines, HasTab{info}, stream));
+    K2H_TRY(hipMemcpyAsync(&nrec, nsel, 8, hipMemcpyDeviceToHost, stream));
+    K2H_TRY(hipStreamSynchronize(stream));
+    if (e == hipSuccess && recs && nrec && nrec <= cap) {
+      tsv_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, rl, nrec, recs);
+      e = hipGetLastError();
+    }
+  } else if (e == hipSuccess && format == K2H_AMD_IMPORT_MDBM) {
+    // header: five getline calls; the fifth must extract exactly "HEADER=END"
+    static const char kEnd[] = "HEADER=END";
+    uint64_t hb = 0, he = 0, body = 0;
+    bool ok = nlines >= 5;
+    if (ok) {
+      uint64_t pos[5] = {0, 0, 0, 0, 0};
+      const uint64_t m = nnl < 5 ? nnl : 5;
+      if (m) K2H_TRY(hipMemcpyAsync(pos, nl, m * 8, hipMemcpyDeviceToHost, stream));
+      K2H_TRY(hipStreamSynchronize(stream));
+      hb = pos[3] + 1;
+      he = nnl >= 5 ? pos[4] : size;  // the fifth line may end at EOF
+      body = nnl >= 5 ? pos[4] + 1 : size;
+      char hdr[sizeof kEnd] = {0};
+      ok = he - hb == sizeof kEnd - 1;
+      if (ok) K2H_TRY(hipMemcpyAsync(hdr, f + hb, sizeof kEnd - 1, hipMemcpyDeviceToHost, stream));
+      K2H_TRY(hipStreamSynchronize(stream));
+      ok = ok && memcmp(hdr, kEnd, sizeof kEnd - 1) == 0;
+    }
+    if (e == hipSuccess && !ok) rc = K2H_AMD_EINVAL;  // k2himport: "error: not a mdbm file."
+    if (e == hipSuccess && ok) {
+      nrec = nlines > 5 ? (nlines - 5 + 1) / 2 : 0;
+      if (recs && nrec && nrec <= cap) {
+        mdbm_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, nlines, nrec, body,
+                                                                          recs);
+        e = hipGetLastError();
+      }
+    }
+  }
+  K2H_TRY(hipStreamSynchronize(stream));
+#undef K2H_TRY
+  for (void* p : {(void*)bcnt, (void*)bbase, (void*)nl, (void*)rl, (void*)nsel, (void*)info, tmp})
+    if (p) (void)hipFreeAsync(p, stream);
+  *herr = e;
+  if (e != hipSuccess) return K2H_AMD_EHIP;
+  if (rc != K2H_AMD_OK) return rc;
+  *count = nrec;
+  return (recs && nrec > cap) ? K2H_AMD_EINVAL : K2H_AMD_OK;
+}
+
+hipError_t launch_import_prehash(const void* file, const k2h_amd_import_rec* recs, uint64_t n, uint64_t seed,
+                                 uint64_t* h1, uint64_t* h2, int variant, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  uint64_t* sl = nullptr;
+  hipError_t e = hipMallocAsync((void**)&sl, 2 * n * 8, stream);
+  if (e != hipSuccess) return e;
+  split_keys_kernel<<<blocks_for(n), kThreads, 0, stream>>>(recs, n, sl, sl + n);
+  e = hipGetLastError();
+  // every key as the C string Set stores: key bytes + NUL
+  if (e == hipSuccess) e = launch_ranges(file, sl, sl + n, n, seed, true, h1, h2, variant, stream);
+  hipError_t g = hipFreeAsync(sl, stream);
+  return e != hipSuccess ? e : g;
+}
+
+}  // namespace k2h

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/k2hash_amd.h"
+
 namespace k2h {
 
 constexpr uint64_t kSeedBuiltinValue = 14695981039346656037ULL;  // lib/k2hashfunc.cc:51
@@ -140,6 +142,13 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
 // Keys at arbitrary (start, length) ranges (k2h_ranges.hip); cstr: hash key + NUL.
 hipError_t launch_ranges(const void* base, const uint64_t* starts, const uint64_t* lens, uint64_t n, uint64_t seed,
                          bool cstr, uint64_t* h1, uint64_t* h2, int variant, hipStream_t stream);
+
+// k2himport inputs already in device memory (k2h_import_dev.hip).  launch_import_scan
+// returns a K2H_AMD_* code (the HIP error in *herr) and synchronises the stream.
+int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
+                       uint64_t* count, hipStream_t stream, hipError_t* herr);
+hipError_t launch_import_prehash(const void* file, const k2h_amd_import_rec* recs, uint64_t n, uint64_t seed,
+                                 uint64_t* h1, uint64_t* h2, int variant, hipStream_t stream);
 
 // S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).
 struct SpadTable {

@@ -90,3 +90,102 @@ def test_prehash_equals_cstr_ranges(cuda, fixture):
     torch.cuda.synchronize()
     assert np.array_equal(g1.cpu().numpy().view(np.uint64), h1)
     assert np.array_equal(g2.cpu().numpy().view(np.uint64), h2)
+
+
+# ------------------------------------------------- GPU: device-resident scan
+def _dev_scan_np(cuda, data, fmt, shift=0):
+    """Device scan of `data` placed `shift` bytes into a device buffer (unaligned bases)."""
+    import torch
+    buf = torch.zeros(len(data) + shift, dtype=torch.uint8, device=cuda)
+    if data:
+        buf[shift:] = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda)
+    f = buf[shift:]
+    recs = archive.import_scan_device(f, fmt)
+    torch.cuda.synchronize()
+    out = np.zeros(recs.shape[0], archive.IMPORT_DTYPE)
+    if recs.shape[0]:
+        a = recs.cpu().numpy().view(np.uint64)
+        for i, k in enumerate(archive.IMPORT_DTYPE.names):
+            out[k] = a[:, i]
+    return f, recs, out
+
+
+@pytest.mark.gpu
+def test_device_scan_matches_host_scan_fixtures(cuda, fixture):
+    """k2h_amd_import_scan_device reports the same records (offsets and C-string
+    lengths) as the host scanner, and hashes them as the reference does."""
+    for name in _cases(fixture):
+        exp = fixture[name]
+        data = (INPUTS / name).read_bytes()
+        if exp["error"]:
+            with pytest.raises(Exception):
+                _dev_scan_np(cuda, data, _fmt(name))
+            continue
+        f, recs, got = _dev_scan_np(cuda, data, _fmt(name))
+        assert np.array_equal(got, archive.import_scan(data, _fmt(name))), name
+        if recs.shape[0]:
+            h1, h2 = archive.import_prehash_device(f, recs)
+            assert [int(x) for x in h1.cpu().numpy().view(np.uint64)] == [u64(e["h1"]) for e in exp["records"]], name
+            assert [int(x) for x in h2.cpu().numpy().view(np.uint64)] == [u64(e["h2"]) for e in exp["records"]], name
+
+
+def _fuzz_file(rng, size, fmt):
+    # few symbols so TABs, newlines, NULs and no-TAB lines are all frequent
+    alphabet = np.frombuffer(b"ab\t\n\x00c\xff", np.uint8)
+    p = np.array([0.3, 0.25, 0.12, 0.18, 0.05, 0.05, 0.05])
+    body = alphabet[rng.choice(alphabet.size, size=size, p=p)].tobytes()
+    if fmt == "mdbm":
+        return b"format=print\ntype=btree\nmdbm_pagesize=4096\nmdbm_pagecount=1\nHEADER=END\n" + body
+    return body
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["tsv", "mdbm"])
+def test_device_scan_fuzz(cuda, fmt):
+    """Random files over a small alphabet (keys across newlines, values with TABs and
+    NULs, every EOF shape), sizes across the 64-byte thread span and 16 KiB block
+    boundaries, and unaligned device bases: device scan == host scan."""
+    rng = np.random.default_rng(0x6B32 + (fmt == "mdbm"))
+    sizes = list(range(0, 80)) + [127, 128, 129, 16383, 16384, 16385, 40000, 200001]
+    for k, size in enumerate(sizes):
+        data = _fuzz_file(rng, size, fmt)
+        shift = k % 5
+        _, _, got = _dev_scan_np(cuda, data, fmt, shift)
+        assert np.array_equal(got, archive.import_scan(data, fmt)), (fmt, size, shift)
+    # EOF shapes of the mdbm header itself
+    if fmt == "mdbm":
+        hdr = b"a\nb\nc\nd\nHEADER=END"
+        for data in (hdr, hdr + b"\n", hdr + b"\nk", hdr + b"\nk\n", hdr + b"\nk\nv", hdr + b"\nk\nv\nk2"):
+            _, _, got = _dev_scan_np(cuda, data, fmt)
+            assert np.array_equal(got, archive.import_scan(data, fmt)), data
+        for bad in (b"", b"a\nb\nc\nd\n", b"a\nb\nc\nd\nHEADER=EN\n", b"a\nb\nc\nd\nHEADER=END \n"):
+            with pytest.raises(Exception):
+                _dev_scan_np(cuda, bad, fmt)
+
+
+@pytest.mark.gpu
+def test_device_scan_and_prehash_large(cuda):
+    """1M-record TSV (keys 1-64 B, values 0-200 B): device scan and device prehash equal
+    the host scan and the host prehash."""
+    import torch
+    rng = np.random.default_rng(7)
+    n = 1 << 20
+    kl = rng.integers(1, 65, n)
+    vl = rng.integers(0, 201, n)
+    ln = kl + vl + 2
+    off = np.concatenate([[0], np.cumsum(ln)])
+    data = rng.integers(32, 127, int(off[-1]), dtype=np.uint8)
+    data[off[:-1] + kl] = 9
+    data[off[1:] - 1] = 10
+    f = torch.from_numpy(data).to(cuda)
+    recs = archive.import_scan_device(f)
+    h1, h2 = archive.import_prehash_device(f, recs)
+    torch.cuda.synchronize()
+    host = archive.import_scan(data.tobytes())
+    assert recs.shape[0] == n == host.size
+    a = recs.cpu().numpy().view(np.uint64)
+    assert np.array_equal(a[:, 0], host["key_off"]) and np.array_equal(a[:, 1], host["key_len"])
+    assert np.array_equal(a[:, 2], host["val_off"]) and np.array_equal(a[:, 3], host["val_len"])
+    e1, e2 = archive.import_prehash(data.tobytes(), host)
+    assert np.array_equal(h1.cpu().numpy().view(np.uint64), e1)
+    assert np.array_equal(h2.cpu().numpy().view(np.uint64), e2)
