@@ -221,11 +221,13 @@ int k2h_amd_import_prehash_host(const void* file, uint64_t size, const k2h_amd_i
  * a TAB (TSV) or every second line after the header (mdbm), found by parallel passes
  * (k2hash_amd/csrc/k2h_import_dev.hip).  Same records, same errors as
  * k2h_amd_import_scan; synchronises `stream`.  k2h_amd_import_prehash hashes every
- * record's key as key + NUL from the device-resident file (async on `stream`). */
+ * record's key as key + NUL straight from the device-resident file, one lane per
+ * record (async on `stream`); a record whose key range is not inside [0, size) gets
+ * h1 = h2 = 0 and nothing outside the file is read. */
 int k2h_amd_import_scan_device(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
                                uint64_t* count, void* stream);
-int k2h_amd_import_prehash(const void* file, const k2h_amd_import_rec* recs, uint64_t n, uint64_t* h1, uint64_t* h2,
-                           uint32_t flags, void* stream);
+int k2h_amd_import_prehash(const void* file, uint64_t size, const k2h_amd_import_rec* recs, uint64_t n, uint64_t* h1,
+                           uint64_t* h2, uint32_t flags, void* stream);
 
 /* Identity / diagnostics. */
 const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */

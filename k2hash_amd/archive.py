@@ -130,13 +130,18 @@ def import_scan_device(file, fmt: str = "tsv", stream=None):
     lib = _native.batch_lib()
     fp = ctypes.c_void_p(file.data_ptr() or 1)
     cnt = ctypes.c_uint64()
-    _native.check(lib.k2h_amd_import_scan_device(fp, file.numel(), code, None, 0, ctypes.byref(cnt),
-                                                 _stream_handle(stream)))
-    recs = torch.empty((cnt.value, 4), dtype=torch.int64, device=file.device)
-    if cnt.value:
-        _native.check(lib.k2h_amd_import_scan_device(fp, file.numel(), code, _dev_ptr(recs), cnt.value,
-                                                     ctypes.byref(cnt), _stream_handle(stream)))
-    return recs
+    # one pass when the guess holds (records of >= 64 bytes on average); otherwise the
+    # call reports the count with K2H_AMD_EINVAL and a second pass fills exact storage
+    cap = max(1024, file.numel() // 64)
+    recs = torch.empty((cap, 4), dtype=torch.int64, device=file.device)
+    rc = lib.k2h_amd_import_scan_device(fp, file.numel(), code, _dev_ptr(recs), cap, ctypes.byref(cnt),
+                                        _stream_handle(stream))
+    if rc == _native.K2H_AMD_EINVAL and cnt.value > cap:
+        recs = torch.empty((cnt.value, 4), dtype=torch.int64, device=file.device)
+        rc = lib.k2h_amd_import_scan_device(fp, file.numel(), code, _dev_ptr(recs), cnt.value, ctypes.byref(cnt),
+                                            _stream_handle(stream))
+    _native.check(rc)
+    return recs[: cnt.value]
 
 
 def import_prehash_device(file, recs, std_fnv: bool = False, stream=None):
@@ -151,6 +156,6 @@ def import_prehash_device(file, recs, std_fnv: bool = False, stream=None):
     h1 = torch.empty(n, dtype=torch.int64, device=file.device)
     h2 = torch.empty(n, dtype=torch.int64, device=file.device)
     _native.check(_native.batch_lib().k2h_amd_import_prehash(
-        ctypes.c_void_p(file.data_ptr() or 1), _dev_ptr(recs), n, _dev_ptr(h1), _dev_ptr(h2),
+        ctypes.c_void_p(file.data_ptr() or 1), file.numel(), _dev_ptr(recs), n, _dev_ptr(h1), _dev_ptr(h2),
         FLAG_STD_FNV if std_fnv else 0, _stream_handle(stream)))
     return h1, h2

@@ -428,12 +428,12 @@ __attribute__((visibility("default"))) int k2h_amd_import_scan_device(const void
   return rc == K2H_AMD_OK ? rc : fail(rc, "import_scan_device: not a mdbm file, or more records than cap");
 }
 
-__attribute__((visibility("default"))) int k2h_amd_import_prehash(const void* file, const k2h_amd_import_rec* recs,
-                                                                  uint64_t n, uint64_t* h1, uint64_t* h2,
+__attribute__((visibility("default"))) int k2h_amd_import_prehash(const void* file, uint64_t size,
+                                                                  const k2h_amd_import_rec* recs, uint64_t n, uint64_t* h1, uint64_t* h2,
                                                                   uint32_t flags, void* stream) {
   if (n == 0) return K2H_AMD_OK;
   if (!file || !recs || !h1) return fail(K2H_AMD_EINVAL, "import_prehash: NULL file/recs/h1");
-  hipError_t e = k2h::launch_import_prehash(file, recs, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream);
+  hipError_t e = k2h::launch_import_prehash(file, size, recs, n, seed_for(flags), h1, h2, (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_import_prehash", e);
 }
 

@@ -18,7 +18,8 @@
 // pairs; the EOF rules of the host scanner (an empty value after a key line that ends
 // the file with '\n', the previous record's value after a key line that ends at EOF).
 //
-// Traffic: the file is read three times (count, positions, lines); outputs are 8 B per
+// Traffic: the file is read twice (pass 1: newline count and span state per block;
+// pass 2: newline positions and per-line TAB / NUL positions, written directly); outputs are 8 B per
 // line plus 32 B per record.  Every pass is a streaming read.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -26,6 +27,7 @@
 #include <string.h>
 
 #include "../../include/k2hash_amd.h"
+#include "k2h_fnv_device.h"
 #include "k2h_kernels.h"
 
 namespace k2h {
@@ -67,53 +69,6 @@ __device__ inline void load_span(const uint8_t* f, uint64_t size, uint64_t b, ui
   }
 }
 
-__global__ __launch_bounds__(kThreads) void nl_count_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                            uint64_t* __restrict__ block_cnt) {
-  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
-  uint32_t c = 0;
-  if (b < size) {
-    uint32_t w[16];
-    load_span(f, size, b, w);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c += __popc(eq_mask(w[k], 0x0A0A0A0Au));
-  }
-  typedef hipcub::BlockReduce<uint32_t, kThreads> Reduce;
-  __shared__ typename Reduce::TempStorage tmp;
-  uint32_t s = Reduce(tmp).Sum(c);
-  if (threadIdx.x == 0) block_cnt[blockIdx.x] = s;  // widened for the scan
-}
-
-// block_base = exclusive scan of block_cnt
-__global__ __launch_bounds__(kThreads) void nl_write_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                            const uint64_t* __restrict__ block_base,
-                                                            uint64_t* __restrict__ nl) {
-  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
-  uint32_t w[16];
-  uint32_t c = 0;
-  if (b < size) {
-    load_span(f, size, b, w);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      w[k] = eq_mask(w[k], 0x0A0A0A0Au);
-      c += __popc(w[k]);
-    }
-  }
-  typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
-  __shared__ typename Scan::TempStorage tmp;
-  uint32_t o;
-  Scan(tmp).ExclusiveSum(c, o);
-  if (!c) return;
-  uint64_t* out = nl + block_base[blockIdx.x] + o;
-  for (int k = 0; k < 16; ++k) {
-    uint32_t m = w[k];
-    while (m) {
-      int bit = __builtin_ctz(m);
-      *out++ = b + 4 * k + (bit >> 3);
-      m &= m - 1;
-    }
-  }
-}
-
 struct LineInfo {
   uint64_t tab;       // first TAB in the line, or kNone
   uint64_t nul;       // first NUL in the line (anywhere), or kNone
@@ -125,47 +80,122 @@ __device__ inline uint64_t line_end(const uint64_t* nl, uint64_t nnl, uint64_t s
   return j < nnl ? nl[j] : size;
 }
 
-// One thread per line: its first TAB and first NUL before / after that TAB.
-__global__ __launch_bounds__(kThreads) void line_info_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                             const uint64_t* __restrict__ nl, uint64_t nnl,
-                                                             uint64_t nlines, LineInfo* __restrict__ info) {
-  const uint64_t j = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (j >= nlines) return;
-  const uint64_t lb = line_begin(nl, j), le = line_end(nl, nnl, size, j);
-  LineInfo r{kNone, kNone, kNone};
-  uint64_t i = lb;
-  // head bytes up to a 4-byte boundary, then words, then the tail
-  for (; i < le && ((uintptr_t)(f + i) & 3); ++i) {
-    uint8_t c = f[i];
-    if (c == 0) {
-      if (r.nul == kNone) r.nul = i;
-      if (r.tab != kNone && r.nul_tab == kNone) r.nul_tab = i;
-    } else if (c == 9 && r.tab == kNone) r.tab = i;
+// State of the line that is open at some point of the file, summarised over a span of
+// bytes: whether the span holds a newline, and since its last newline (or its start)
+// whether a TAB, a NUL, and a NUL after a TAB were seen.  Combining spans in file order
+// is associative (a segmented "or"), so blocks and threads get their incoming state
+// from scans: a thread then knows, for every TAB / NUL it holds, whether it is the
+// first of its kind in its line.
+enum : uint32_t { kHasNl = 1, kTab = 2, kNul = 4, kNulTab = 8 };
+struct SpanOp {
+  __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const {
+    if (b & kHasNl) return b;
+    return (a & kHasNl) | ((a | b) & (kTab | kNul | kNulTab)) | (((a & kTab) && (b & kNul)) ? kNulTab : 0);
   }
-  for (; i + 4 <= le; i += 4) {
-    const uint32_t w = *reinterpret_cast<const uint32_t*>(f + i);
-    uint32_t mz = eq_mask(w, 0), mt = eq_mask(w, 0x09090909u);
-    if (!(mz | mt)) continue;
-    for (int k = 0; k < 4; ++k) {
-      const uint32_t bit = 0x80u << (8 * k);
-      if (mz & bit) {
-        if (r.nul == kNone) r.nul = i + k;
-        if (r.tab != kNone && r.nul_tab == kNone) r.nul_tab = i + k;
-      } else if ((mt & bit) && r.tab == kNone) r.tab = i + k;
+};
+
+struct SpanMasks {
+  uint32_t nl[16], ev[16];  // newline bytes; newline / TAB / NUL bytes (bit 7 of each)
+};
+
+__device__ inline void span_masks(const uint32_t w[16], SpanMasks& m) {
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    m.nl[k] = eq_mask(w[k], 0x0A0A0A0Au);
+    m.ev[k] = m.nl[k] | eq_mask(w[k], 0x09090909u) | eq_mask(w[k], 0);
+  }
+}
+
+// Walk the span's events in byte order from state `st`; with Write, record each newline
+// position and each line's first TAB / first NUL / first NUL after its first TAB.
+template <bool Write>
+__device__ inline uint32_t span_walk(const uint32_t w[16], const SpanMasks& m, uint64_t b, uint32_t st,
+                                     uint64_t line, uint64_t* __restrict__ nl, LineInfo* __restrict__ info) {
+  for (int k = 0; k < 16; ++k) {
+    uint32_t x = m.ev[k];
+    while (x) {
+      const int bit = __builtin_ctz(x);
+      x &= x - 1;
+      const uint64_t pos = b + 4 * k + (bit >> 3);
+      if (m.nl[k] & (1u << bit)) {
+        if constexpr (Write) nl[line] = pos;
+        ++line;
+        st = kHasNl;
+      } else if (((w[k] >> (bit - 7)) & 0xFFu) == 9) {  // TAB
+        if (!(st & kTab)) {
+          if constexpr (Write) info[line].tab = pos;
+          st |= kTab;
+        }
+      } else {  // NUL
+        if (!(st & kNul)) {
+          if constexpr (Write) info[line].nul = pos;
+          st |= kNul;
+        }
+        if ((st & kTab) && !(st & kNulTab)) {
+          if constexpr (Write) info[line].nul_tab = pos;
+          st |= kNulTab;
+        }
+      }
     }
-    if (r.tab != kNone && r.nul_tab != kNone) {  // nothing more to learn
-      i = le;
-      break;
-    }
   }
-  for (; i < le; ++i) {
-    uint8_t c = f[i];
-    if (c == 0) {
-      if (r.nul == kNone) r.nul = i;
-      if (r.tab != kNone && r.nul_tab == kNone) r.nul_tab = i;
-    } else if (c == 9 && r.tab == kNone) r.tab = i;
+  return st;
+}
+
+// Pass 1: newline count and span state per block.
+__global__ __launch_bounds__(kThreads) void span_count_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                              uint64_t* __restrict__ block_cnt,
+                                                              uint32_t* __restrict__ block_state) {
+  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
+  uint32_t c = 0, st = 0;
+  if (b < size) {
+    uint32_t w[16];
+    SpanMasks m;
+    load_span(f, size, b, w);
+    span_masks(w, m);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c += __popc(m.nl[k]);
+    st = span_walk<false>(w, m, b, 0, 0, nullptr, nullptr);
   }
-  info[j] = r;
+  typedef hipcub::BlockReduce<uint32_t, kThreads> Reduce;
+  typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
+  __shared__ union {
+    typename Reduce::TempStorage r;
+    typename Scan::TempStorage s;
+  } tmp;
+  const uint32_t sum = Reduce(tmp.r).Sum(c);
+  __syncthreads();
+  uint32_t inc;
+  Scan(tmp.s).InclusiveScan(st, inc, SpanOp());
+  if (threadIdx.x == kThreads - 1) block_state[blockIdx.x] = inc;
+  if (threadIdx.x == 0) block_cnt[blockIdx.x] = sum;
+}
+
+// Pass 2 (block_base / block_in = exclusive scans of pass 1): newline positions in
+// order, and every line's first TAB / NUL / NUL-after-TAB written straight into info.
+__global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                              const uint64_t* __restrict__ block_base,
+                                                              const uint32_t* __restrict__ block_in,
+                                                              uint64_t* __restrict__ nl,
+                                                              LineInfo* __restrict__ info) {
+  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
+  uint32_t w[16];
+  SpanMasks m;
+  uint32_t c = 0, st = 0;
+  if (b < size) {
+    load_span(f, size, b, w);
+    span_masks(w, m);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) c += __popc(m.nl[k]);
+    st = span_walk<false>(w, m, b, 0, 0, nullptr, nullptr);
+  }
+  typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  uint32_t o, in;
+  Scan(tmp).ExclusiveSum(c, o);
+  __syncthreads();
+  Scan(tmp).ExclusiveScan(st, in, block_in[blockIdx.x], SpanOp());
+  if (b >= size) return;
+  span_walk<true>(w, m, b, in, block_base[blockIdx.x] + o, nl, info);
 }
 
 struct HasTab {
@@ -233,13 +263,59 @@ __global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* 
   recs[r] = o;
 }
 
-__global__ __launch_bounds__(kThreads) void split_keys_kernel(const k2h_amd_import_rec* __restrict__ recs, uint64_t n,
-                                                              uint64_t* __restrict__ starts,
-                                                              uint64_t* __restrict__ lens) {
+// One lane per record: the key straight from the file (no gather) as k = ceil(len/16)
+// 16-byte chunks that END at its last byte (the CSR kernels' end-aligned form): chunk 0
+// starts p = 16k - len bytes early with those bytes zeroed, and the state starts at
+// S_p = seed * P^-p, which the p zero bytes (bare multiplies) carry exactly to the seed
+// -- no byte-by-byte tail.  Then the NUL that K2HShm::Set(const char*) hashes with the
+// key (lib/k2hshm.cc:2081-2083): a zero byte is a bare multiply, so h1 = state * P and
+// h2 = state (lib/k2hashfunc.cc:83-85); the empty key is the one-byte "\0", h1 = h2 =
+// seed * P.
+typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
+
+__device__ inline uint4 ld16(const uint8_t* p) {
+  const u32x4_ua v = *reinterpret_cast<const u32x4_ua*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__global__ __launch_bounds__(kThreads) void import_hash_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                               const k2h_amd_import_rec* __restrict__ recs,
+                                                               uint64_t n, SpadTable sp, uint64_t* __restrict__ h1,
+                                                               uint64_t* __restrict__ h2) {
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
-  starts[i] = recs[i].key_off;
-  lens[i] = recs[i].key_len;
+  const uint64_t off = recs[i].key_off, len = recs[i].key_len;
+  if (off > size || len > size - off) {  // not a range of this file: never read past it
+    h1[i] = 0;
+    if (h2) h2[i] = 0;
+    return;
+  }
+  const uint64_t seed = sp.v[0];
+  uint64_t raw = seed;
+  if (len) {
+    const uint64_t k = (len + 15) / 16;
+    const uint32_t p = (uint32_t)(16 * k - len);
+    const uint8_t* c0 = f + off - p;  // chunk 0 (its first p bytes are not the key's)
+    uint4 c;
+    if (off >= p) {
+      c = ld16(c0);
+    } else {  // the key starts the file: no bytes before it to over-read
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t j = p; j < 16; ++j) w[j >> 2] |= (uint32_t)f[off - p + j] << (8 * (j & 3));
+      c = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    // zero bytes [0, p)
+    const uint32_t m0 = p >= 4 ? 0u : ~0u << (8 * p), m1 = p >= 8 ? 0u : p <= 4 ? ~0u : ~0u << (8 * (p - 4));
+    const uint32_t m2 = p >= 12 ? 0u : p <= 8 ? ~0u : ~0u << (8 * (p - 8)), m3 = p <= 12 ? ~0u : ~0u << (8 * (p - 12));
+    c.x &= m0, c.y &= m1, c.z &= m2, c.w &= m3;
+    uint32_t lo = (uint32_t)sp.v[p], hi = (uint32_t)(sp.v[p] >> 32);
+    fnv_chunk16(lo, hi, c);
+    for (uint64_t q = 1; q < k; ++q) fnv_chunk16(lo, hi, ld16(c0 + 16 * q));
+    raw = ((uint64_t)hi << 32) | lo;
+  }
+  const uint64_t a = raw * 1099511628211ULL;  // lib/k2hashfunc.cc:56
+  h1[i] = a;
+  if (h2) h2[i] = len ? raw : a;
 }
 
 unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
@@ -259,7 +335,8 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   LineInfo* info = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
-  uint64_t nnl = 0, nlines = 0, nrec = 0, last_nl = 0;
+  uint32_t *bst = nullptr, *bin = nullptr;
+  uint64_t nnl = 0, nlines = 0, nrec = 0;
   int rc = K2H_AMD_OK;
   hipError_t e = hipSuccess;
 #define K2H_TRY(x) \
@@ -269,28 +346,31 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   if (nblk) {
     K2H_TRY(hipMallocAsync((void**)&bcnt, nblk * 8, stream));
     K2H_TRY(hipMallocAsync((void**)&bbase, (nblk + 1) * 8, stream));
+    K2H_TRY(hipMallocAsync((void**)&bst, nblk * 4, stream));
+    K2H_TRY(hipMallocAsync((void**)&bin, nblk * 4, stream));
     if (e == hipSuccess) {
-      nl_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt);
+      span_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt, bst);
       e = hipGetLastError();
     }
     K2H_TRY(hipMemsetAsync(bbase, 0, 8, stream));
-    K2H_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, tmp_bytes, bcnt, bbase + 1, nblk, stream));
+    size_t t1 = 0, t2 = 0;
+    K2H_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t1, bcnt, bbase + 1, nblk, stream));
+    K2H_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, t2, bst, bin, SpanOp(), 0u, nblk, stream));
+    tmp_bytes = t1 > t2 ? t1 : t2;
     K2H_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
-    K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, tmp_bytes, bcnt, bbase + 1, nblk, stream));
+    K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, bcnt, bbase + 1, nblk, stream));
+    K2H_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, t2, bst, bin, SpanOp(), 0u, nblk, stream));
+    uint8_t last = '\n';
     K2H_TRY(hipMemcpyAsync(&nnl, bbase + nblk, 8, hipMemcpyDeviceToHost, stream));
+    K2H_TRY(hipMemcpyAsync(&last, f + size - 1, 1, hipMemcpyDeviceToHost, stream));
     K2H_TRY(hipStreamSynchronize(stream));
-    K2H_TRY(hipMallocAsync((void**)&nl, (nnl ? nnl : 1) * 8, stream));
-    if (e == hipSuccess && nnl) {
-      nl_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, nl);
-      e = hipGetLastError();
-      K2H_TRY(hipMemcpyAsync(&last_nl, nl + nnl - 1, 8, hipMemcpyDeviceToHost, stream));
-      K2H_TRY(hipStreamSynchronize(stream));
-    }
     // lines: one per newline, plus the bytes after the last newline if any
-    nlines = nnl + ((nnl ? last_nl + 1 : 0) < size ? 1 : 0);
+    nlines = nnl + (last != '\n' ? 1 : 0);
+    K2H_TRY(hipMallocAsync((void**)&nl, (nnl ? nnl : 1) * 8, stream));
     K2H_TRY(hipMallocAsync((void**)&info, (nlines ? nlines : 1) * sizeof(LineInfo), stream));
-    if (e == hipSuccess && nlines) {
-      line_info_kernel<<<blocks_for(nlines), kThreads, 0, stream>>>(f, size, nl, nnl, nlines, info);
+    if (nlines) K2H_TRY(hipMemsetAsync(info, 0xFF, nlines * sizeof(LineInfo), stream));  // kNone
+    if (e == hipSuccess) {
+      span_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, bin, nl, info);
       e = hipGetLastError();
     }
   }
@@ -341,7 +421,7 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   }
   K2H_TRY(hipStreamSynchronize(stream));
 #undef K2H_TRY
-  for (void* p : {(void*)bcnt, (void*)bbase, (void*)nl, (void*)rl, (void*)nsel, (void*)info, tmp})
+  for (void* p : {(void*)bcnt, (void*)bbase, (void*)bst, (void*)bin, (void*)nl, (void*)rl, (void*)nsel, (void*)info, tmp})
     if (p) (void)hipFreeAsync(p, stream);
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;
@@ -350,18 +430,12 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   return (recs && nrec > cap) ? K2H_AMD_EINVAL : K2H_AMD_OK;
 }
 
-hipError_t launch_import_prehash(const void* file, const k2h_amd_import_rec* recs, uint64_t n, uint64_t seed,
-                                 uint64_t* h1, uint64_t* h2, int variant, hipStream_t stream) {
+hipError_t launch_import_prehash(const void* file, uint64_t size, const k2h_amd_import_rec* recs, uint64_t n,
+                                 uint64_t seed, uint64_t* h1, uint64_t* h2, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  uint64_t* sl = nullptr;
-  hipError_t e = hipMallocAsync((void**)&sl, 2 * n * 8, stream);
-  if (e != hipSuccess) return e;
-  split_keys_kernel<<<blocks_for(n), kThreads, 0, stream>>>(recs, n, sl, sl + n);
-  e = hipGetLastError();
-  // every key as the C string Set stores: key bytes + NUL
-  if (e == hipSuccess) e = launch_ranges(file, sl, sl + n, n, seed, true, h1, h2, variant, stream);
-  hipError_t g = hipFreeAsync(sl, stream);
-  return e != hipSuccess ? e : g;
+  import_hash_kernel<<<blocks_for(n), kThreads, 0, stream>>>((const uint8_t*)file, size, recs, n, make_spad(seed),
+                                                              h1, h2);
+  return hipGetLastError();
 }
 
 }  // namespace k2h

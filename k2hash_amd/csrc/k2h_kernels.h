@@ -147,8 +147,8 @@ hipError_t launch_ranges(const void* base, const uint64_t* starts, const uint64_
 // returns a K2H_AMD_* code (the HIP error in *herr) and synchronises the stream.
 int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
                        uint64_t* count, hipStream_t stream, hipError_t* herr);
-hipError_t launch_import_prehash(const void* file, const k2h_amd_import_rec* recs, uint64_t n, uint64_t seed,
-                                 uint64_t* h1, uint64_t* h2, int variant, hipStream_t stream);
+hipError_t launch_import_prehash(const void* file, uint64_t size, const k2h_amd_import_rec* recs, uint64_t n,
+                                 uint64_t seed, uint64_t* h1, uint64_t* h2, hipStream_t stream);
 
 // S_p = seed * P^-p (p = 0..15): start states for end-aligned chunking (k2h_csr.hip).
 struct SpadTable {
