@@ -7,9 +7,12 @@
 // start to the first TAB (across newlines), its value from there to the next '\n'.  So a
 // record ends exactly at the newline of every line that holds a TAB, and the lines with
 // no TAB in front of it belong to its key.  Record ends are therefore a per-line
-// predicate and the loop needs no sequential walk: (1) newline positions by a per-chunk
-// count + scan + ordered write, (2) per line its first TAB and its first NUL (before and
-// after that TAB; keys and values are cut there, c_str()/strlen), (3) the TAB lines
+// predicate and the loop needs no sequential walk: (1) per 16 KiB block, its newline
+// count and its "span state" (newline seen; TAB / NUL / NUL-after-TAB seen since the
+// last newline), scanned across blocks; (2) newline positions in order, and each line's
+// first TAB and first NUL before / after that TAB (keys and values are cut there,
+// c_str()/strlen) written directly, each thread knowing from the scanned state whether
+// an event is the first of its kind in its line; (3) the TAB lines
 // compacted into records.  The bytes after the last newline form a last line whose
 // value ends at EOF; if it holds no TAB the key getline hits EOF and it is dropped,
 // as is a trailing run of newline-terminated lines with no TAB.

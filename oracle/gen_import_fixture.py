@@ -5,7 +5,8 @@
                                       tests/k2himport.cc:74-117 (keys spanning newlines,
                                       empty keys / values, NUL bytes, CR LF, high bytes,
                                       text after the last TAB, bad and short mdbm headers)
-                                      plus a seeded 3000-record TSV
+                                      plus a seeded 3000-record TSV and seeded
+                                      small-alphabet fuzz files (fuzz_*)
   tests/golden/import.json            for each input, what oracle/_ref/gen_import prints:
                                       the records k2himport's own loops produce (libstdc++
                                       getline) and every key hashed by the REFERENCE's
@@ -58,10 +59,26 @@ def random_tsv(n=3000, seed=7):
     return b"".join(lines)
 
 
+def fuzz_inputs(seed=0x6B32):
+    """Small-alphabet files (TAB, newline, NUL, high bytes frequent: keys across lines,
+    values with TABs and NULs, every EOF shape) at sizes around the device scanner's
+    64-byte thread span and 16 KiB block (k2hash_amd/csrc/k2h_import_dev.hip)."""
+    rng = random.Random(seed)
+    alphabet = b"ab\t\n\x00c\xff"
+    weights = [30, 25, 12, 18, 5, 5, 5]
+    out = {}
+    for size in (1, 2, 3, 5, 8, 13, 21, 34, 55, 63, 64, 65, 127, 128, 129, 300, 1000, 4097, 16383, 16384, 16385):
+        out[f"fuzz_{size:05d}.tsv"] = bytes(rng.choices(alphabet, weights, k=size))
+    for size in (0, 1, 2, 3, 5, 8, 13, 64, 65, 300, 4097):
+        out[f"fuzz_{size:05d}.mdbm"] = HDR + bytes(rng.choices(alphabet, weights, k=size))
+    return out
+
+
 def main():
     OUT.mkdir(parents=True, exist_ok=True)
     inputs = dict(INPUTS)
     inputs["random.tsv"] = random_tsv()
+    inputs.update(fuzz_inputs())
     fixture = {"generator": "oracle/_ref/gen_import (tests/k2himport.cc loops, reference lib/k2hashfunc.cc)",
                "inputs": {}}
     for name, data in sorted(inputs.items()):
