@@ -12,8 +12,9 @@
 // last newline), scanned across blocks; (2) newline positions in order, and each line's
 // first TAB and first NUL before / after that TAB (keys and values are cut there,
 // c_str()/strlen) written directly, each thread knowing from the scanned state whether
-// an event is the first of its kind in its line; (3) the TAB lines
-// compacted into records.  The bytes after the last newline form a last line whose
+// an event is the first of its kind in its line; (3) the TAB lines' indices written in
+// order by the same pass (a per-block record count, taken in pass 1 for both possible
+// incoming states, is scanned like the newline count), then one record per TAB line.  The bytes after the last newline form a last line whose
 // value ends at EOF; if it holds no TAB the key getline hits EOF and it is dropped,
 // as is a trailing run of newline-terminated lines with no TAB.
 // mdbm (ConvertfromMdbm, tests/k2himport.cc:95-117).  Five header lines (the fifth
@@ -21,8 +22,9 @@
 // pairs; the EOF rules of the host scanner (an empty value after a key line that ends
 // the file with '\n', the previous record's value after a key line that ends at EOF).
 //
-// Traffic: the file is read twice (pass 1: newline count and span state per block;
-// pass 2: newline positions and per-line TAB / NUL positions, written directly); outputs are 8 B per
+// Traffic: the file is read twice (pass 1: newline count, span state and record-end
+// count per block; pass 2: newline positions, per-line TAB / NUL positions and the
+// record-ending lines, written directly; a count-only TSV call stops after pass 1); outputs are 8 B per
 // line plus 32 B per record.  Every pass is a streaming read.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
@@ -110,10 +112,21 @@ __device__ inline void span_masks(const uint32_t w[16], SpanMasks& m) {
 }
 
 // Walk the span's events in byte order from state `st`; with Write, record each newline
-// position and each line's first TAB / first NUL / first NUL after its first TAB.
+// position and each line's first TAB / first NUL / first NUL after its first TAB, and
+// (rl != NULL, TSV) the index of every line that ends a record -- a line holding a TAB --
+// at rl[rec++].  Counts the record ends it passes.
+struct Walk {
+  uint32_t st;        // state after the span
+  uint32_t recs;      // newlines that end a TAB line
+  bool first_nl_tab;  // the first newline's line had a TAB (within the span)
+  bool any_nl;
+};
+
 template <bool Write>
-__device__ inline uint32_t span_walk(const uint32_t w[16], const SpanMasks& m, uint64_t b, uint32_t st,
-                                     uint64_t line, uint64_t* __restrict__ nl, LineInfo* __restrict__ info) {
+__device__ inline Walk span_walk(const uint32_t w[16], const SpanMasks& m, uint64_t b, uint32_t st, uint64_t line,
+                                 uint64_t* __restrict__ nl, LineInfo* __restrict__ info, uint64_t* __restrict__ rl,
+                                 uint64_t rec) {
+  Walk r{st, 0, false, false};
   for (int k = 0; k < 16; ++k) {
     uint32_t x = m.ev[k];
     while (x) {
@@ -122,6 +135,14 @@ __device__ inline uint32_t span_walk(const uint32_t w[16], const SpanMasks& m, u
       const uint64_t pos = b + 4 * k + (bit >> 3);
       if (m.nl[k] & (1u << bit)) {
         if constexpr (Write) nl[line] = pos;
+        if (!r.any_nl) r.first_nl_tab = (st & kTab) != 0;
+        r.any_nl = true;
+        if (st & kTab) {
+          if constexpr (Write) {
+            if (rl) rl[rec++] = line;
+          }
+          ++r.recs;
+        }
         ++line;
         st = kHasNl;
       } else if (((w[k] >> (bit - 7)) & 0xFFu) == 9) {  // TAB
@@ -141,15 +162,25 @@ __device__ inline uint32_t span_walk(const uint32_t w[16], const SpanMasks& m, u
       }
     }
   }
-  return st;
+  r.st = st;
+  return r;
 }
 
-// Pass 1: newline count and span state per block.
+// Record ends in a span given whether the line open at its start already holds a TAB
+// (only the span's first newline depends on it).
+__device__ inline uint32_t span_recs(const Walk& s, uint32_t in) {
+  return s.recs + ((in & kTab) && s.any_nl && !s.first_nl_tab ? 1u : 0u);
+}
+
+// Pass 1: per block, the newline count, the span state, and the record-end count for
+// both possible incoming states (low / high 32 bits: open line without / with a TAB).
 __global__ __launch_bounds__(kThreads) void span_count_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                               uint64_t* __restrict__ block_cnt,
-                                                              uint32_t* __restrict__ block_state) {
+                                                              uint32_t* __restrict__ block_state,
+                                                              uint64_t* __restrict__ block_recs) {
   const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
-  uint32_t c = 0, st = 0;
+  uint32_t c = 0;
+  Walk s{0, 0, false, false};
   if (b < size) {
     uint32_t w[16];
     SpanMasks m;
@@ -157,54 +188,79 @@ __global__ __launch_bounds__(kThreads) void span_count_kernel(const uint8_t* __r
     span_masks(w, m);
 #pragma unroll
     for (int k = 0; k < 16; ++k) c += __popc(m.nl[k]);
-    st = span_walk<false>(w, m, b, 0, 0, nullptr, nullptr);
+    s = span_walk<false>(w, m, b, 0, 0, nullptr, nullptr, nullptr, 0);
   }
-  typedef hipcub::BlockReduce<uint32_t, kThreads> Reduce;
+  typedef hipcub::BlockReduce<uint64_t, kThreads> Reduce;
   typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
   __shared__ union {
     typename Reduce::TempStorage r;
     typename Scan::TempStorage s;
   } tmp;
-  const uint32_t sum = Reduce(tmp.r).Sum(c);
+  uint32_t inc, in0, in1;
+  Scan(tmp.s).InclusiveScan(s.st, inc, SpanOp());
   __syncthreads();
-  uint32_t inc;
-  Scan(tmp.s).InclusiveScan(st, inc, SpanOp());
+  Scan(tmp.s).ExclusiveScan(s.st, in0, 0u, SpanOp());
+  __syncthreads();
+  Scan(tmp.s).ExclusiveScan(s.st, in1, (uint32_t)kTab, SpanOp());
+  __syncthreads();
+  const uint64_t packed = (uint64_t)c | ((uint64_t)span_recs(s, in0) << 32);
+  const uint64_t sum = Reduce(tmp.r).Sum(packed);
+  __syncthreads();
+  const uint64_t r1 = Reduce(tmp.r).Sum((uint64_t)span_recs(s, in1));
   if (threadIdx.x == kThreads - 1) block_state[blockIdx.x] = inc;
-  if (threadIdx.x == 0) block_cnt[blockIdx.x] = sum;
+  if (threadIdx.x == 0) {
+    block_cnt[blockIdx.x] = sum & 0xFFFFFFFFu;
+    block_recs[blockIdx.x] = (sum >> 32) | (r1 << 32);
+  }
 }
 
-// Pass 2 (block_base / block_in = exclusive scans of pass 1): newline positions in
-// order, and every line's first TAB / NUL / NUL-after-TAB written straight into info.
+// Record-end count of each block under its real incoming state.
+__global__ __launch_bounds__(kThreads) void block_recs_kernel(const uint64_t* __restrict__ both,
+                                                              const uint32_t* __restrict__ block_in, uint64_t nblk,
+                                                              uint64_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= nblk) return;
+  out[i] = (block_in[i] & kTab) ? both[i] >> 32 : both[i] & 0xFFFFFFFFu;
+}
+
+// Pass 2 (block_base / block_in / rec_base = exclusive scans of pass 1): newline
+// positions in order, every line's first TAB / NUL / NUL-after-TAB written straight
+// into info, and (TSV) the record-ending line indices into rl -- including the bytes
+// after the last newline when they hold a TAB (a record whose value ends at EOF).
 __global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                               const uint64_t* __restrict__ block_base,
                                                               const uint32_t* __restrict__ block_in,
+                                                              const uint64_t* __restrict__ rec_base,
                                                               uint64_t* __restrict__ nl,
-                                                              LineInfo* __restrict__ info) {
+                                                              LineInfo* __restrict__ info,
+                                                              uint64_t* __restrict__ rl) {
   const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
   uint32_t w[16];
   SpanMasks m;
-  uint32_t c = 0, st = 0;
+  uint32_t c = 0;
+  Walk s{0, 0, false, false};
   if (b < size) {
     load_span(f, size, b, w);
     span_masks(w, m);
 #pragma unroll
     for (int k = 0; k < 16; ++k) c += __popc(m.nl[k]);
-    st = span_walk<false>(w, m, b, 0, 0, nullptr, nullptr);
+    s = span_walk<false>(w, m, b, 0, 0, nullptr, nullptr, nullptr, 0);
   }
   typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
   __shared__ typename Scan::TempStorage tmp;
-  uint32_t o, in;
+  uint32_t o, in, ro;
   Scan(tmp).ExclusiveSum(c, o);
   __syncthreads();
-  Scan(tmp).ExclusiveScan(st, in, block_in[blockIdx.x], SpanOp());
+  Scan(tmp).ExclusiveScan(s.st, in, block_in[blockIdx.x], SpanOp());
+  __syncthreads();
+  Scan(tmp).ExclusiveSum(span_recs(s, in), ro);
   if (b >= size) return;
-  span_walk<true>(w, m, b, in, block_base[blockIdx.x] + o, nl, info);
+  const uint64_t line = block_base[blockIdx.x] + o, rec = rec_base[blockIdx.x] + ro;
+  const Walk e = span_walk<true>(w, m, b, in, line, nl, info, rl, rec);
+  // the thread holding the last byte: an open last line with a TAB is a record
+  if (rl && b + kBytesPerThread >= size && f[size - 1] != '\n' && (e.st & kTab))
+    rl[rec + e.recs] = line + c;
 }
-
-struct HasTab {
-  const LineInfo* info;
-  __host__ __device__ bool operator()(const uint64_t& j) const { return info[j].tab != kNone; }
-};
 
 // TSV: record r ends at TAB line rl[r]; its key starts after the previous TAB line.
 __global__ __launch_bounds__(kThreads) void tsv_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
@@ -334,7 +390,7 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   const uint64_t nblk = size ? (size + kChunk - 1) / kChunk : 0;
   if (nblk > 0x7FFFFFFFull) return K2H_AMD_EINVAL;
   uint64_t* bcnt = nullptr;
-  uint64_t *bbase = nullptr, *nl = nullptr, *rl = nullptr, *nsel = nullptr;
+  uint64_t *bbase = nullptr, *nl = nullptr, *rl = nullptr, *brec2 = nullptr, *brec = nullptr, *rbase = nullptr;
   LineInfo* info = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
@@ -346,16 +402,21 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   do {             \
     if (e == hipSuccess) e = (x); \
   } while (0)
+  const bool tsv = format == K2H_AMD_IMPORT_TSV;
   if (nblk) {
     K2H_TRY(hipMallocAsync((void**)&bcnt, nblk * 8, stream));
     K2H_TRY(hipMallocAsync((void**)&bbase, (nblk + 1) * 8, stream));
     K2H_TRY(hipMallocAsync((void**)&bst, nblk * 4, stream));
     K2H_TRY(hipMallocAsync((void**)&bin, nblk * 4, stream));
+    K2H_TRY(hipMallocAsync((void**)&brec2, nblk * 8, stream));
+    K2H_TRY(hipMallocAsync((void**)&brec, nblk * 8, stream));
+    K2H_TRY(hipMallocAsync((void**)&rbase, (nblk + 1) * 8, stream));
     if (e == hipSuccess) {
-      span_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt, bst);
+      span_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt, bst, brec2);
       e = hipGetLastError();
     }
     K2H_TRY(hipMemsetAsync(bbase, 0, 8, stream));
+    K2H_TRY(hipMemsetAsync(rbase, 0, 8, stream));
     size_t t1 = 0, t2 = 0;
     K2H_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t1, bcnt, bbase + 1, nblk, stream));
     K2H_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, t2, bst, bin, SpanOp(), 0u, nblk, stream));
@@ -363,33 +424,39 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
     K2H_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
     K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, bcnt, bbase + 1, nblk, stream));
     K2H_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, t2, bst, bin, SpanOp(), 0u, nblk, stream));
+    if (e == hipSuccess) {
+      block_recs_kernel<<<blocks_for(nblk), kThreads, 0, stream>>>(brec2, bin, nblk, brec);
+      e = hipGetLastError();
+    }
+    K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, brec, rbase + 1, nblk, stream));  // same shape as bcnt
     uint8_t last = '\n';
+    uint32_t st_last = 0, in_last = 0;
+    uint64_t nrec_nl = 0;
     K2H_TRY(hipMemcpyAsync(&nnl, bbase + nblk, 8, hipMemcpyDeviceToHost, stream));
+    K2H_TRY(hipMemcpyAsync(&nrec_nl, rbase + nblk, 8, hipMemcpyDeviceToHost, stream));
+    K2H_TRY(hipMemcpyAsync(&st_last, bst + nblk - 1, 4, hipMemcpyDeviceToHost, stream));
+    K2H_TRY(hipMemcpyAsync(&in_last, bin + nblk - 1, 4, hipMemcpyDeviceToHost, stream));
     K2H_TRY(hipMemcpyAsync(&last, f + size - 1, 1, hipMemcpyDeviceToHost, stream));
     K2H_TRY(hipStreamSynchronize(stream));
     // lines: one per newline, plus the bytes after the last newline if any
     nlines = nnl + (last != '\n' ? 1 : 0);
-    K2H_TRY(hipMallocAsync((void**)&nl, (nnl ? nnl : 1) * 8, stream));
-    K2H_TRY(hipMallocAsync((void**)&info, (nlines ? nlines : 1) * sizeof(LineInfo), stream));
-    if (nlines) K2H_TRY(hipMemsetAsync(info, 0xFF, nlines * sizeof(LineInfo), stream));  // kNone
-    if (e == hipSuccess) {
-      span_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, bin, nl, info);
-      e = hipGetLastError();
+    // TSV records: newlines ending a TAB line, plus an open last line holding a TAB
+    if (tsv) nrec = nrec_nl + ((last != '\n' && (SpanOp()(in_last, st_last) & kTab)) ? 1 : 0);
+    // TSV needs pass 2 only to fill records; mdbm always (its header check reads nl)
+    const bool pass2 = !tsv || (recs && nrec && nrec <= cap);
+    if (pass2) {
+      K2H_TRY(hipMallocAsync((void**)&nl, (nnl ? nnl : 1) * 8, stream));
+      K2H_TRY(hipMallocAsync((void**)&info, (nlines ? nlines : 1) * sizeof(LineInfo), stream));
+      if (tsv) K2H_TRY(hipMallocAsync((void**)&rl, nrec * 8, stream));
+      if (nlines) K2H_TRY(hipMemsetAsync(info, 0xFF, nlines * sizeof(LineInfo), stream));  // kNone
+      if (e == hipSuccess) {
+        span_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, bin, rbase, nl, info, rl);
+        e = hipGetLastError();
+      }
     }
   }
-  if (e == hipSuccess && format == K2H_AMD_IMPORT_TSV && nlines) {
-    if (tmp) (void)hipFreeAsync(tmp, stream);
-    tmp = nullptr;
-    tmp_bytes = 0;
-    K2H_TRY(hipMallocAsync((void**)&rl, nlines * 8, stream));
-    K2H_TRY(hipMallocAsync((void**)&nsel, 8, stream));
-    hipcub::CountingInputIterator<uint64_t> it(0);
-    K2H_TRY(hipcub::DeviceSelect::If(nullptr, tmp_bytes, it, rl, nsel, nlines, HasTab{info}, stream));
-    K2H_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
-    K2H_TRY(hipcub::DeviceSelect::If(tmp, tmp_bytes, it, rl, nsel, nlines, HasTab{info}, stream));
-    K2H_TRY(hipMemcpyAsync(&nrec, nsel, 8, hipMemcpyDeviceToHost, stream));
-    K2H_TRY(hipStreamSynchronize(stream));
-    if (e == hipSuccess && recs && nrec && nrec <= cap) {
+  if (e == hipSuccess && tsv) {
+    if (recs && nrec && nrec <= cap) {
       tsv_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, rl, nrec, recs);
       e = hipGetLastError();
     }
@@ -424,7 +491,8 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   }
   K2H_TRY(hipStreamSynchronize(stream));
 #undef K2H_TRY
-  for (void* p : {(void*)bcnt, (void*)bbase, (void*)bst, (void*)bin, (void*)nl, (void*)rl, (void*)nsel, (void*)info, tmp})
+  for (void* p : {(void*)bcnt, (void*)bbase, (void*)bst, (void*)bin, (void*)brec2, (void*)brec, (void*)rbase, (void*)nl,
+                  (void*)rl, (void*)info, tmp})
     if (p) (void)hipFreeAsync(p, stream);
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;
