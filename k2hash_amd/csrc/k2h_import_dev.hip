@@ -99,6 +99,12 @@ struct SpanOp {
   }
 };
 
+struct CountStateOp {  // (newline count << 8 | span state) pairs, combined in file order
+  __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const {
+    return (((a >> 8) + (b >> 8)) << 8) | SpanOp()(a & 0xFFu, b & 0xFFu);
+  }
+};
+
 struct SpanMasks {
   uint32_t nl[16], ev[16];  // newline bytes; newline / TAB / NUL bytes (bit 7 of each)
 };
@@ -196,21 +202,21 @@ __global__ __launch_bounds__(kThreads) void span_count_kernel(const uint8_t* __r
     typename Reduce::TempStorage r;
     typename Scan::TempStorage s;
   } tmp;
-  uint32_t inc, in0, in1;
-  Scan(tmp.s).InclusiveScan(s.st, inc, SpanOp());
-  __syncthreads();
+  // incoming state assuming the block starts on a line with no TAB; assuming one with a
+  // TAB differs only before the block's first newline: in1 has kTab iff in0 has, or no
+  // newline precedes the thread
+  uint32_t in0;
   Scan(tmp.s).ExclusiveScan(s.st, in0, 0u, SpanOp());
   __syncthreads();
-  Scan(tmp.s).ExclusiveScan(s.st, in1, (uint32_t)kTab, SpanOp());
-  __syncthreads();
-  const uint64_t packed = (uint64_t)c | ((uint64_t)span_recs(s, in0) << 32);
+  const uint32_t in1 = (in0 & kHasNl) ? in0 : (in0 | kTab);
+  // newline count and both record counts fit 21 bits each (<= 16384 per block)
+  const uint64_t packed = (uint64_t)c | ((uint64_t)span_recs(s, in0) << 21) | ((uint64_t)span_recs(s, in1) << 42);
   const uint64_t sum = Reduce(tmp.r).Sum(packed);
-  __syncthreads();
-  const uint64_t r1 = Reduce(tmp.r).Sum((uint64_t)span_recs(s, in1));
-  if (threadIdx.x == kThreads - 1) block_state[blockIdx.x] = inc;
+  if (threadIdx.x == kThreads - 1) block_state[blockIdx.x] = SpanOp()(in0, s.st);
   if (threadIdx.x == 0) {
-    block_cnt[blockIdx.x] = sum & 0xFFFFFFFFu;
-    block_recs[blockIdx.x] = (sum >> 32) | (r1 << 32);
+    constexpr uint64_t m21 = (1ull << 21) - 1;
+    block_cnt[blockIdx.x] = sum & m21;
+    block_recs[blockIdx.x] = ((sum >> 21) & m21) | (((sum >> 42) & m21) << 32);
   }
 }
 
@@ -248,11 +254,11 @@ __global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __r
   }
   typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
   __shared__ typename Scan::TempStorage tmp;
-  uint32_t o, in, ro;
-  Scan(tmp).ExclusiveSum(c, o);
+  // newline count (<= 2^14 per block) above the 4 state bits: one scan for both
+  uint32_t co, ro;
+  Scan(tmp).ExclusiveScan((c << 8) | s.st, co, block_in[blockIdx.x], CountStateOp());
   __syncthreads();
-  Scan(tmp).ExclusiveScan(s.st, in, block_in[blockIdx.x], SpanOp());
-  __syncthreads();
+  const uint32_t o = co >> 8, in = co & 0xFFu;
   Scan(tmp).ExclusiveSum(span_recs(s, in), ro);
   if (b >= size) return;
   const uint64_t line = block_base[blockIdx.x] + o, rec = rec_base[blockIdx.x] + ro;
