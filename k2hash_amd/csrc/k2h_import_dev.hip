@@ -105,16 +105,11 @@ struct CountStateOp {  // (newline count << 8 | span state) pairs, combined in f
   }
 };
 
-struct SpanMasks {
-  uint32_t nl[16], ev[16];  // newline bytes; newline / TAB / NUL bytes (bit 7 of each)
-};
-
-__device__ inline void span_masks(const uint32_t w[16], SpanMasks& m) {
+__device__ inline uint32_t nl_count(const uint32_t w[16]) {
+  uint32_t c = 0;
 #pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    m.nl[k] = eq_mask(w[k], 0x0A0A0A0Au);
-    m.ev[k] = m.nl[k] | eq_mask(w[k], 0x09090909u) | eq_mask(w[k], 0);
-  }
+  for (int k = 0; k < 16; ++k) c += __popc(eq_mask(w[k], 0x0A0A0A0Au));
+  return c;
 }
 
 // Walk the span's events in byte order from state `st`; with Write, record each newline
@@ -129,17 +124,20 @@ struct Walk {
 };
 
 template <bool Write>
-__device__ inline Walk span_walk(const uint32_t w[16], const SpanMasks& m, uint64_t b, uint32_t st, uint64_t line,
+__device__ inline Walk span_walk(const uint32_t w[16], uint64_t b, uint32_t st, uint64_t line,
                                  uint64_t* __restrict__ nl, LineInfo* __restrict__ info, uint64_t* __restrict__ rl,
                                  uint64_t rec) {
   Walk r{st, 0, false, false};
+#pragma unroll
   for (int k = 0; k < 16; ++k) {
-    uint32_t x = m.ev[k];
+    // masks per word, not kept for the span: fewer live registers, more waves
+    const uint32_t mnl = eq_mask(w[k], 0x0A0A0A0Au);
+    uint32_t x = mnl | eq_mask(w[k], 0x09090909u) | eq_mask(w[k], 0);
     while (x) {
       const int bit = __builtin_ctz(x);
       x &= x - 1;
       const uint64_t pos = b + 4 * k + (bit >> 3);
-      if (m.nl[k] & (1u << bit)) {
+      if (mnl & (1u << bit)) {
         if constexpr (Write) nl[line] = pos;
         if (!r.any_nl) r.first_nl_tab = (st & kTab) != 0;
         r.any_nl = true;
@@ -189,12 +187,9 @@ __global__ __launch_bounds__(kThreads) void span_count_kernel(const uint8_t* __r
   Walk s{0, 0, false, false};
   if (b < size) {
     uint32_t w[16];
-    SpanMasks m;
     load_span(f, size, b, w);
-    span_masks(w, m);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c += __popc(m.nl[k]);
-    s = span_walk<false>(w, m, b, 0, 0, nullptr, nullptr, nullptr, 0);
+    c = nl_count(w);
+    s = span_walk<false>(w, b, 0, 0, nullptr, nullptr, nullptr, 0);
   }
   typedef hipcub::BlockReduce<uint64_t, kThreads> Reduce;
   typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
@@ -242,15 +237,12 @@ __global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __r
                                                               uint64_t* __restrict__ rl) {
   const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
   uint32_t w[16];
-  SpanMasks m;
   uint32_t c = 0;
   Walk s{0, 0, false, false};
   if (b < size) {
     load_span(f, size, b, w);
-    span_masks(w, m);
-#pragma unroll
-    for (int k = 0; k < 16; ++k) c += __popc(m.nl[k]);
-    s = span_walk<false>(w, m, b, 0, 0, nullptr, nullptr, nullptr, 0);
+    c = nl_count(w);
+    s = span_walk<false>(w, b, 0, 0, nullptr, nullptr, nullptr, 0);
   }
   typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
   __shared__ typename Scan::TempStorage tmp;
@@ -262,7 +254,7 @@ __global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __r
   Scan(tmp).ExclusiveSum(span_recs(s, in), ro);
   if (b >= size) return;
   const uint64_t line = block_base[blockIdx.x] + o, rec = rec_base[blockIdx.x] + ro;
-  const Walk e = span_walk<true>(w, m, b, in, line, nl, info, rl, rec);
+  const Walk e = span_walk<true>(w, b, in, line, nl, info, rl, rec);
   // the thread holding the last byte: an open last line with a TAB is a record
   if (rl && b + kBytesPerThread >= size && f[size - 1] != '\n' && (e.st & kTab))
     rl[rec + e.recs] = line + c;
