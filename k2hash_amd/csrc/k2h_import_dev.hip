@@ -385,7 +385,9 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   const uint8_t* f = (const uint8_t*)file;
   *herr = hipSuccess;
   *count = 0;
-  const uint64_t nblk = size ? (size + kChunk - 1) / kChunk : 0;
+  // an empty file: no records (TSV), or no header (mdbm: "not a mdbm file"); no device work
+  if (size == 0) return format == K2H_AMD_IMPORT_TSV ? K2H_AMD_OK : K2H_AMD_EINVAL;
+  const uint64_t nblk = (size + kChunk - 1) / kChunk;
   if (nblk > 0x7FFFFFFFull) return K2H_AMD_EINVAL;
   uint64_t* bcnt = nullptr;
   uint64_t *bbase = nullptr, *nl = nullptr, *rl = nullptr, *brec2 = nullptr, *brec = nullptr, *rbase = nullptr;

@@ -146,6 +146,17 @@ def test_batch_abi_argument_errors():
                                   None) == _native.K2H_AMD_EINVAL  # overflow
     assert b"h1" in lib.k2h_amd_strerror(_native.K2H_AMD_EINVAL) or lib.k2h_amd_strerror(-1)
     assert lib.k2h_amd_version().startswith(b"k2hash_amd")
+    # device k2himport scan / prehash: argument checks precede any device work
+    cnt = ctypes.c_uint64(99)
+    assert lib.k2h_amd_import_scan_device(ctypes.c_void_p(16), 10, 0, None, 0, None, None) == _native.K2H_AMD_EINVAL
+    assert lib.k2h_amd_import_scan_device(None, 10, 0, None, 0, ctypes.byref(cnt), None) == _native.K2H_AMD_EINVAL
+    assert lib.k2h_amd_import_scan_device(ctypes.c_void_p(16), 10, 7, None, 0, ctypes.byref(cnt),
+                                          None) == _native.K2H_AMD_EINVAL  # not TSV / mdbm
+    assert lib.k2h_amd_import_scan_device(None, 0, 0, None, 0, ctypes.byref(cnt), None) == _native.K2H_AMD_OK
+    assert cnt.value == 0  # empty TSV: no records, no device work
+    assert lib.k2h_amd_import_prehash(None, 0, None, 0, None, None, 0, None) == _native.K2H_AMD_OK  # n == 0
+    assert lib.k2h_amd_import_prehash(None, 0, None, 3, ctypes.c_void_p(8), None, 0,
+                                      None) == _native.K2H_AMD_EINVAL
 
 
 def test_host_api_null_buffers_without_gpu():
