@@ -228,6 +228,12 @@ int k2h_amd_import_scan_device(const void* file, uint64_t size, int format, k2h_
                                uint64_t* count, void* stream);
 int k2h_amd_import_prehash(const void* file, uint64_t size, const k2h_amd_import_rec* recs, uint64_t n, uint64_t* h1,
                            uint64_t* h2, uint32_t flags, void* stream);
+/* Both in one call: the records and, from the same kernel, h1 / h2 (h2 may be NULL) of
+ * every record's key + NUL -- the prehash without a second pass over the records.  h1
+ * and h2 need room for cap entries; count / cap / errors as k2h_amd_import_scan_device. */
+int k2h_amd_import_scan_prehash_device(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs,
+                                       uint64_t cap, uint64_t* count, uint64_t* h1, uint64_t* h2, uint32_t flags,
+                                       void* stream);
 
 /* Identity / diagnostics. */
 const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */

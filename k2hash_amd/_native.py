@@ -49,6 +49,8 @@ SIGNATURES = {
     "k2h_amd_import_prehash_host": (ctypes.c_int, [_p, _u64, _p, _u64, _p, _p, ctypes.c_uint32, ctypes.c_int]),
     "k2h_amd_import_scan_device": (ctypes.c_int, [_p, _u64, ctypes.c_int, _p, _u64, _p, _p]),
     "k2h_amd_import_prehash": (ctypes.c_int, [_p, _u64, _p, _u64, _p, _p, ctypes.c_uint32, _p]),
+    "k2h_amd_import_scan_prehash_device": (ctypes.c_int, [_p, _u64, ctypes.c_int, _p, _u64, _p, _p, _p,
+                                                          ctypes.c_uint32, _p]),
     "k2h_amd_version": (ctypes.c_char_p, []),
     "k2h_amd_strerror": (ctypes.c_char_p, [ctypes.c_int]),
     "k2h_amd_set_variant": (ctypes.c_int, [ctypes.c_int]),

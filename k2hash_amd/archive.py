@@ -159,3 +159,29 @@ def import_prehash_device(file, recs, std_fnv: bool = False, stream=None):
         ctypes.c_void_p(file.data_ptr() or 1), file.numel(), _dev_ptr(recs), n, _dev_ptr(h1), _dev_ptr(h2),
         FLAG_STD_FNV if std_fnv else 0, _stream_handle(stream)))
     return h1, h2
+
+
+def import_scan_prehash_device(file, fmt: str = "tsv", std_fnv: bool = False, stream=None):
+    """import_scan_device + import_prehash_device in one call: the records and their keys'
+    (h1, h2) from the same kernel (k2h_amd_import_scan_prehash_device)."""
+    torch = _torch()
+    _check_dev(file, "file", torch.uint8)
+    code = {"tsv": IMPORT_TSV, "mdbm": IMPORT_MDBM}[fmt]
+    lib = _native.batch_lib()
+    fp = ctypes.c_void_p(file.data_ptr() or 1)
+    flags = FLAG_STD_FNV if std_fnv else 0
+    cnt = ctypes.c_uint64()
+    rc = 0
+    cap = max(1024, file.numel() // 64)  # as import_scan_device: one pass when the guess holds
+    for _ in range(2):
+        recs = torch.empty((cap, 4), dtype=torch.int64, device=file.device)
+        h1 = torch.empty(cap, dtype=torch.int64, device=file.device)
+        h2 = torch.empty(cap, dtype=torch.int64, device=file.device)
+        rc = lib.k2h_amd_import_scan_prehash_device(fp, file.numel(), code, _dev_ptr(recs), cap, ctypes.byref(cnt),
+                                                    _dev_ptr(h1), _dev_ptr(h2), flags, _stream_handle(stream))
+        if not (rc == _native.K2H_AMD_EINVAL and cnt.value > cap):
+            break
+        cap = cnt.value
+    _native.check(rc)
+    n = cnt.value
+    return recs[:n], h1[:n], h2[:n]

@@ -428,6 +428,19 @@ __attribute__((visibility("default"))) int k2h_amd_import_scan_device(const void
   return rc == K2H_AMD_OK ? rc : fail(rc, "import_scan_device: not a mdbm file, or more records than cap");
 }
 
+__attribute__((visibility("default"))) int k2h_amd_import_scan_prehash_device(
+    const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count, uint64_t* h1,
+    uint64_t* h2, uint32_t flags, void* stream) {
+  if (!count || (size && !file) || (format != K2H_AMD_IMPORT_TSV && format != K2H_AMD_IMPORT_MDBM))
+    return fail(K2H_AMD_EINVAL, "import_scan_prehash_device: NULL count/file or bad format");
+  if (recs && cap && !h1) return fail(K2H_AMD_EINVAL, "import_scan_prehash_device: NULL h1");
+  hipError_t e = hipSuccess;
+  int rc = k2h::launch_import_scan(file, size, format, recs, cap, count, (hipStream_t)stream, &e, h1, h2,
+                                   seed_for(flags));
+  if (rc == K2H_AMD_EHIP) return fail(rc, "launch_import_scan", e);
+  return rc == K2H_AMD_OK ? rc : fail(rc, "import_scan_prehash_device: not a mdbm file, or more records than cap");
+}
+
 __attribute__((visibility("default"))) int k2h_amd_import_prehash(const void* file, uint64_t size,
                                                                   const k2h_amd_import_rec* recs, uint64_t n, uint64_t* h1, uint64_t* h2,
                                                                   uint32_t flags, void* stream) {

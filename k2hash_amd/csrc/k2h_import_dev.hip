@@ -260,11 +260,69 @@ __global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __r
     rl[rec + e.recs] = line + c;
 }
 
+// One lane per record: the key straight from the file (no gather) as k = ceil(len/16)
+// 16-byte chunks that END at its last byte (the CSR kernels' end-aligned form): chunk 0
+// starts p = 16k - len bytes early with those bytes zeroed, and the state starts at
+// S_p = seed * P^-p, which the p zero bytes (bare multiplies) carry exactly to the seed
+// -- no byte-by-byte tail.  Then the NUL that K2HShm::Set(const char*) hashes with the
+// key (lib/k2hshm.cc:2081-2083): a zero byte is a bare multiply, so h1 = state * P and
+// h2 = state (lib/k2hashfunc.cc:83-85); the empty key is the one-byte "\0", h1 = h2 =
+// seed * P.
+typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
+
+__device__ inline uint4 ld16(const uint8_t* p) {
+  const u32x4_ua v = *reinterpret_cast<const u32x4_ua*>(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ inline void hash_cstr(const uint8_t* __restrict__ f, uint64_t off, uint64_t len, const SpadTable& sp,
+                                 uint64_t& h1, uint64_t& h2) {
+  uint64_t raw = sp.v[0];  // the seed
+  if (len) {
+    const uint64_t k = (len + 15) / 16;
+    const uint32_t p = (uint32_t)(16 * k - len);
+    const uint8_t* c0 = f + off - p;  // chunk 0 (its first p bytes are not the key's)
+    uint4 c;
+    if (off >= p) {
+      c = ld16(c0);
+    } else {  // the key starts the file: no bytes before it to over-read
+      uint32_t w[4] = {0, 0, 0, 0};
+      for (uint32_t j = p; j < 16; ++j) w[j >> 2] |= (uint32_t)f[off - p + j] << (8 * (j & 3));
+      c = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    // zero bytes [0, p)
+    const uint32_t m0 = p >= 4 ? 0u : ~0u << (8 * p), m1 = p >= 8 ? 0u : p <= 4 ? ~0u : ~0u << (8 * (p - 4));
+    const uint32_t m2 = p >= 12 ? 0u : p <= 8 ? ~0u : ~0u << (8 * (p - 8)), m3 = p <= 12 ? ~0u : ~0u << (8 * (p - 12));
+    c.x &= m0, c.y &= m1, c.z &= m2, c.w &= m3;
+    uint32_t lo = (uint32_t)sp.v[p], hi = (uint32_t)(sp.v[p] >> 32);
+    fnv_chunk16(lo, hi, c);
+    for (uint64_t q = 1; q < k; ++q) fnv_chunk16(lo, hi, ld16(c0 + 16 * q));
+    raw = ((uint64_t)hi << 32) | lo;
+  }
+  h1 = raw * 1099511628211ULL;  // lib/k2hashfunc.cc:56
+  h2 = len ? raw : h1;
+}
+
+__global__ __launch_bounds__(kThreads) void import_hash_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                               const k2h_amd_import_rec* __restrict__ recs,
+                                                               uint64_t n, SpadTable sp, uint64_t* __restrict__ h1,
+                                                               uint64_t* __restrict__ h2) {
+  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t off = recs[i].key_off, len = recs[i].key_len;
+  uint64_t a = 0, b = 0;
+  if (off <= size && len <= size - off) hash_cstr(f, off, len, sp, a, b);  // else: never read past the file
+  h1[i] = a;
+  if (h2) h2[i] = b;
+}
+
 // TSV: record r ends at TAB line rl[r]; its key starts after the previous TAB line.
 __global__ __launch_bounds__(kThreads) void tsv_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
                                                                uint64_t size, const LineInfo* __restrict__ info,
                                                                const uint64_t* __restrict__ rl, uint64_t nrec,
-                                                               k2h_amd_import_rec* __restrict__ recs) {
+                                                               k2h_amd_import_rec* __restrict__ recs,
+                                                               const uint8_t* __restrict__ f, SpadTable sp,
+                                                               uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
   const uint64_t r = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   if (r >= nrec) return;
   const uint64_t j1 = rl[r], j0 = r ? rl[r - 1] + 1 : 0;
@@ -284,13 +342,21 @@ __global__ __launch_bounds__(kThreads) void tsv_records_kernel(const uint64_t* _
   o.val_off = vb;
   o.val_len = ve - vb;  // a TAB that ends the file: getline fails, empty value at EOF
   recs[r] = o;
+  if (h1) {  // fused prehash: the key as the C string Set stores
+    uint64_t a, b;
+    hash_cstr(f, o.key_off, o.key_len, sp, a, b);
+    h1[r] = a;
+    if (h2) h2[r] = b;
+  }
 }
 
 // mdbm: key line 5 + 2r, value line 6 + 2r (see the header comment for the EOF rules).
 __global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
                                                                 uint64_t size, const LineInfo* __restrict__ info,
                                                                 uint64_t nlines, uint64_t nrec, uint64_t body,
-                                                                k2h_amd_import_rec* __restrict__ recs) {
+                                                                k2h_amd_import_rec* __restrict__ recs,
+                                                                const uint8_t* __restrict__ f, SpadTable sp,
+                                                                uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
   const uint64_t r = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   if (r >= nrec) return;
   const uint64_t kl = 5 + 2 * r;
@@ -318,61 +384,12 @@ __global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* 
     o.val_len = 0;
   }
   recs[r] = o;
-}
-
-// One lane per record: the key straight from the file (no gather) as k = ceil(len/16)
-// 16-byte chunks that END at its last byte (the CSR kernels' end-aligned form): chunk 0
-// starts p = 16k - len bytes early with those bytes zeroed, and the state starts at
-// S_p = seed * P^-p, which the p zero bytes (bare multiplies) carry exactly to the seed
-// -- no byte-by-byte tail.  Then the NUL that K2HShm::Set(const char*) hashes with the
-// key (lib/k2hshm.cc:2081-2083): a zero byte is a bare multiply, so h1 = state * P and
-// h2 = state (lib/k2hashfunc.cc:83-85); the empty key is the one-byte "\0", h1 = h2 =
-// seed * P.
-typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
-
-__device__ inline uint4 ld16(const uint8_t* p) {
-  const u32x4_ua v = *reinterpret_cast<const u32x4_ua*>(p);
-  return make_uint4(v.x, v.y, v.z, v.w);
-}
-
-__global__ __launch_bounds__(kThreads) void import_hash_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                               const k2h_amd_import_rec* __restrict__ recs,
-                                                               uint64_t n, SpadTable sp, uint64_t* __restrict__ h1,
-                                                               uint64_t* __restrict__ h2) {
-  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t off = recs[i].key_off, len = recs[i].key_len;
-  if (off > size || len > size - off) {  // not a range of this file: never read past it
-    h1[i] = 0;
-    if (h2) h2[i] = 0;
-    return;
+  if (h1) {  // fused prehash: the key as the C string Set stores
+    uint64_t a, b;
+    hash_cstr(f, o.key_off, o.key_len, sp, a, b);
+    h1[r] = a;
+    if (h2) h2[r] = b;
   }
-  const uint64_t seed = sp.v[0];
-  uint64_t raw = seed;
-  if (len) {
-    const uint64_t k = (len + 15) / 16;
-    const uint32_t p = (uint32_t)(16 * k - len);
-    const uint8_t* c0 = f + off - p;  // chunk 0 (its first p bytes are not the key's)
-    uint4 c;
-    if (off >= p) {
-      c = ld16(c0);
-    } else {  // the key starts the file: no bytes before it to over-read
-      uint32_t w[4] = {0, 0, 0, 0};
-      for (uint32_t j = p; j < 16; ++j) w[j >> 2] |= (uint32_t)f[off - p + j] << (8 * (j & 3));
-      c = make_uint4(w[0], w[1], w[2], w[3]);
-    }
-    // zero bytes [0, p)
-    const uint32_t m0 = p >= 4 ? 0u : ~0u << (8 * p), m1 = p >= 8 ? 0u : p <= 4 ? ~0u : ~0u << (8 * (p - 4));
-    const uint32_t m2 = p >= 12 ? 0u : p <= 8 ? ~0u : ~0u << (8 * (p - 8)), m3 = p <= 12 ? ~0u : ~0u << (8 * (p - 12));
-    c.x &= m0, c.y &= m1, c.z &= m2, c.w &= m3;
-    uint32_t lo = (uint32_t)sp.v[p], hi = (uint32_t)(sp.v[p] >> 32);
-    fnv_chunk16(lo, hi, c);
-    for (uint64_t q = 1; q < k; ++q) fnv_chunk16(lo, hi, ld16(c0 + 16 * q));
-    raw = ((uint64_t)hi << 32) | lo;
-  }
-  const uint64_t a = raw * 1099511628211ULL;  // lib/k2hashfunc.cc:56
-  h1[i] = a;
-  if (h2) h2[i] = len ? raw : a;
 }
 
 unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
@@ -381,7 +398,8 @@ unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThread
 
 // Returns K2H_AMD_* codes (the HIP error, if any, in *herr).
 int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
-                       uint64_t* count, hipStream_t stream, hipError_t* herr) {
+                       uint64_t* count, hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2,
+                       uint64_t seed) {
   const uint8_t* f = (const uint8_t*)file;
   *herr = hipSuccess;
   *count = 0;
@@ -457,7 +475,8 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   }
   if (e == hipSuccess && tsv) {
     if (recs && nrec && nrec <= cap) {
-      tsv_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, rl, nrec, recs);
+      tsv_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, rl, nrec, recs, f,
+                                                                    make_spad(seed), h1, h2);
       e = hipGetLastError();
     }
   } else if (e == hipSuccess && format == K2H_AMD_IMPORT_MDBM) {
@@ -484,7 +503,7 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
       nrec = nlines > 5 ? (nlines - 5 + 1) / 2 : 0;
       if (recs && nrec && nrec <= cap) {
         mdbm_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, nlines, nrec, body,
-                                                                          recs);
+                                                                          recs, f, make_spad(seed), h1, h2);
         e = hipGetLastError();
       }
     }

@@ -145,8 +145,10 @@ hipError_t launch_ranges(const void* base, const uint64_t* starts, const uint64_
 
 // k2himport inputs already in device memory (k2h_import_dev.hip).  launch_import_scan
 // returns a K2H_AMD_* code (the HIP error in *herr) and synchronises the stream.
+// h1 != NULL: each written record's key is also hashed (key + NUL) by the same kernel.
 int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
-                       uint64_t* count, hipStream_t stream, hipError_t* herr);
+                       uint64_t* count, hipStream_t stream, hipError_t* herr, uint64_t* h1 = nullptr,
+                       uint64_t* h2 = nullptr, uint64_t seed = 0);
 hipError_t launch_import_prehash(const void* file, uint64_t size, const k2h_amd_import_rec* recs, uint64_t n,
                                  uint64_t seed, uint64_t* h1, uint64_t* h2, hipStream_t stream);
 

@@ -164,6 +164,30 @@ def test_device_scan_fuzz(cuda, fmt):
 
 
 @pytest.mark.gpu
+def test_fused_scan_prehash_matches_reference(cuda, fixture):
+    """k2h_amd_import_scan_prehash_device: same records as the host scan and the
+    reference's hashes, from one call (both the one-pass and the grow-and-retry paths)."""
+    import torch
+    for name in _cases(fixture):
+        exp = fixture[name]
+        data = (INPUTS / name).read_bytes()
+        f = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda)
+        if exp["error"]:
+            with pytest.raises(Exception):
+                archive.import_scan_prehash_device(f, _fmt(name))
+            continue
+        recs, h1, h2 = archive.import_scan_prehash_device(f, _fmt(name))
+        torch.cuda.synchronize()
+        host = archive.import_scan(data, _fmt(name))
+        a = recs.cpu().numpy().view(np.uint64)
+        assert a.shape[0] == host.size, name
+        for i, k in enumerate(archive.IMPORT_DTYPE.names):
+            assert np.array_equal(a[:, i], host[k]), (name, k)
+        assert [int(x) for x in h1.cpu().numpy().view(np.uint64)] == [u64(e["h1"]) for e in exp["records"]], name
+        assert [int(x) for x in h2.cpu().numpy().view(np.uint64)] == [u64(e["h2"]) for e in exp["records"]], name
+
+
+@pytest.mark.gpu
 def test_device_scan_and_prehash_large(cuda):
     """1M-record TSV (keys 1-64 B, values 0-200 B): device scan and device prehash equal
     the host scan and the host prehash."""
@@ -189,3 +213,6 @@ def test_device_scan_and_prehash_large(cuda):
     e1, e2 = archive.import_prehash(data.tobytes(), host)
     assert np.array_equal(h1.cpu().numpy().view(np.uint64), e1)
     assert np.array_equal(h2.cpu().numpy().view(np.uint64), e2)
+    frecs, f1, f2 = archive.import_scan_prehash_device(f)
+    torch.cuda.synchronize()
+    assert torch.equal(frecs, recs) and torch.equal(f1, h1) and torch.equal(f2, h2)

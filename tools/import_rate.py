@@ -57,6 +57,13 @@ def main():
         tp.append(t2 - t1)
     assert recs.shape[0] == n
     scan_s, pre_s = float(np.median(ts)), float(np.median(tp))
+    tf = []
+    for _ in range(a.reps + 1):
+        t0 = time.perf_counter()
+        archive.import_scan_prehash_device(f)
+        torch.cuda.synchronize()
+        tf.append(time.perf_counter() - t0)
+    fused_s = float(np.median(tf[1:]))
 
     t0 = time.perf_counter()
     host = archive.import_scan(data)
@@ -67,6 +74,7 @@ def main():
         "workload": f"{n} TSV records, keys 8-64 B, values 0-200 B, {size} bytes",
         "device": {"scan_s": scan_s, "prehash_s": pre_s, "records_per_s": n / (scan_s + pre_s),
                    "file_GB_per_s": size / (scan_s + pre_s) / 1e9, "scan_file_GB_per_s": size / scan_s / 1e9},
+        "device_fused": {"s": fused_s, "records_per_s": n / fused_s, "file_GB_per_s": size / fused_s / 1e9},
         "host": {"scan_s": t1 - t0, "prehash_s": t2 - t1, "records_per_s": n / (t2 - t0),
                  "file_GB_per_s": size / (t2 - t0) / 1e9, "scan_threads": 1},
     }))
