@@ -31,6 +31,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "../../include/k2hash_amd.h"
 #include "k2h_fnv_device.h"
 #include "k2h_kernels.h"
@@ -396,6 +398,42 @@ unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThread
 
 }  // namespace
 
+__global__ void scan_summary_kernel(const uint8_t* __restrict__ f, uint64_t size, const uint64_t* __restrict__ bbase,
+                                    const uint64_t* __restrict__ rbase, const uint32_t* __restrict__ bst,
+                                    const uint32_t* __restrict__ bin, uint64_t nblk, uint64_t* __restrict__ out) {
+  out[0] = bbase[nblk];
+  out[1] = rbase[nblk];
+  out[2] = f[size - 1];
+  out[3] = SpanOp()(bin[nblk - 1], bst[nblk - 1]);
+}
+
+// Scratch for the per-call temporaries: a library-private stream-ordered pool per device
+// whose release threshold keeps freed memory mapped (the default pool returns it at every
+// synchronisation, so each call would map its line / record arrays again).  The pool
+// holds at most the peak of one call's temporaries.
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
+  constexpr int kMaxDev = 64;
+  static hipMemPool_t pools[kMaxDev] = {};
+  static std::once_flag once[kMaxDev];
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  if (dev < 0 || dev >= kMaxDev) return hipMallocAsync(p, bytes, stream);
+  std::call_once(once[dev], [dev] {
+    hipMemPoolProps props = {};
+    props.allocType = hipMemAllocationTypePinned;
+    props.handleTypes = hipMemHandleTypeNone;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    hipMemPool_t pool = nullptr;
+    if (hipMemPoolCreate(&pool, &props) != hipSuccess) return;
+    uint64_t keep = ~0ull;
+    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    pools[dev] = pool;
+  });
+  return pools[dev] ? hipMallocFromPoolAsync(p, bytes, pools[dev], stream) : hipMallocAsync(p, bytes, stream);
+}
+
 // Returns K2H_AMD_* codes (the HIP error, if any, in *herr).
 int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
                        uint64_t* count, hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2,
@@ -422,13 +460,13 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   } while (0)
   const bool tsv = format == K2H_AMD_IMPORT_TSV;
   if (nblk) {
-    K2H_TRY(hipMallocAsync((void**)&bcnt, nblk * 8, stream));
-    K2H_TRY(hipMallocAsync((void**)&bbase, (nblk + 1) * 8, stream));
-    K2H_TRY(hipMallocAsync((void**)&bst, nblk * 4, stream));
-    K2H_TRY(hipMallocAsync((void**)&bin, nblk * 4, stream));
-    K2H_TRY(hipMallocAsync((void**)&brec2, nblk * 8, stream));
-    K2H_TRY(hipMallocAsync((void**)&brec, nblk * 8, stream));
-    K2H_TRY(hipMallocAsync((void**)&rbase, (nblk + 1) * 8, stream));
+    K2H_TRY(scratch_alloc((void**)&bcnt, nblk * 8, stream));
+    K2H_TRY(scratch_alloc((void**)&bbase, (nblk + 1) * 8, stream));
+    K2H_TRY(scratch_alloc((void**)&bst, nblk * 4, stream));
+    K2H_TRY(scratch_alloc((void**)&bin, nblk * 4, stream));
+    K2H_TRY(scratch_alloc((void**)&brec2, nblk * 8, stream));
+    K2H_TRY(scratch_alloc((void**)&brec, nblk * 8, stream));
+    K2H_TRY(scratch_alloc((void**)&rbase, (nblk + 1) * 8, stream));
     if (e == hipSuccess) {
       span_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt, bst, brec2);
       e = hipGetLastError();
@@ -439,7 +477,7 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
     K2H_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t1, bcnt, bbase + 1, nblk, stream));
     K2H_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, t2, bst, bin, SpanOp(), 0u, nblk, stream));
     tmp_bytes = t1 > t2 ? t1 : t2;
-    K2H_TRY(hipMallocAsync(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
+    K2H_TRY(scratch_alloc(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
     K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, bcnt, bbase + 1, nblk, stream));
     K2H_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, t2, bst, bin, SpanOp(), 0u, nblk, stream));
     if (e == hipSuccess) {
@@ -447,25 +485,31 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
       e = hipGetLastError();
     }
     K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, brec, rbase + 1, nblk, stream));  // same shape as bcnt
-    uint8_t last = '\n';
-    uint32_t st_last = 0, in_last = 0;
-    uint64_t nrec_nl = 0;
-    K2H_TRY(hipMemcpyAsync(&nnl, bbase + nblk, 8, hipMemcpyDeviceToHost, stream));
-    K2H_TRY(hipMemcpyAsync(&nrec_nl, rbase + nblk, 8, hipMemcpyDeviceToHost, stream));
-    K2H_TRY(hipMemcpyAsync(&st_last, bst + nblk - 1, 4, hipMemcpyDeviceToHost, stream));
-    K2H_TRY(hipMemcpyAsync(&in_last, bin + nblk - 1, 4, hipMemcpyDeviceToHost, stream));
-    K2H_TRY(hipMemcpyAsync(&last, f + size - 1, 1, hipMemcpyDeviceToHost, stream));
+    // one read-back: newline count, newline record ends, last byte, final span state
+    uint64_t sum[4] = {0, 0, '\n', 0};
+    uint64_t* dsum = nullptr;
+    K2H_TRY(scratch_alloc((void**)&dsum, sizeof sum, stream));
+    if (e == hipSuccess) {
+      scan_summary_kernel<<<1, 1, 0, stream>>>(f, size, bbase, rbase, bst, bin, nblk, dsum);
+      e = hipGetLastError();
+    }
+    K2H_TRY(hipMemcpyAsync(sum, dsum, sizeof sum, hipMemcpyDeviceToHost, stream));
     K2H_TRY(hipStreamSynchronize(stream));
+    if (dsum) (void)hipFreeAsync(dsum, stream);
+    nnl = sum[0];
+    const uint64_t nrec_nl = sum[1];
+    const uint8_t last = (uint8_t)sum[2];
+    const uint32_t st_final = (uint32_t)sum[3];
     // lines: one per newline, plus the bytes after the last newline if any
     nlines = nnl + (last != '\n' ? 1 : 0);
     // TSV records: newlines ending a TAB line, plus an open last line holding a TAB
-    if (tsv) nrec = nrec_nl + ((last != '\n' && (SpanOp()(in_last, st_last) & kTab)) ? 1 : 0);
+    if (tsv) nrec = nrec_nl + ((last != '\n' && (st_final & kTab)) ? 1 : 0);
     // TSV needs pass 2 only to fill records; mdbm always (its header check reads nl)
     const bool pass2 = !tsv || (recs && nrec && nrec <= cap);
     if (pass2) {
-      K2H_TRY(hipMallocAsync((void**)&nl, (nnl ? nnl : 1) * 8, stream));
-      K2H_TRY(hipMallocAsync((void**)&info, (nlines ? nlines : 1) * sizeof(LineInfo), stream));
-      if (tsv) K2H_TRY(hipMallocAsync((void**)&rl, nrec * 8, stream));
+      K2H_TRY(scratch_alloc((void**)&nl, (nnl ? nnl : 1) * 8, stream));
+      K2H_TRY(scratch_alloc((void**)&info, (nlines ? nlines : 1) * sizeof(LineInfo), stream));
+      if (tsv) K2H_TRY(scratch_alloc((void**)&rl, nrec * 8, stream));
       if (nlines) K2H_TRY(hipMemsetAsync(info, 0xFF, nlines * sizeof(LineInfo), stream));  // kNone
       if (e == hipSuccess) {
         span_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, bin, rbase, nl, info, rl);
