@@ -1,25 +1,33 @@
 #!/usr/bin/env python3
 """bench.py -- k2hash key-hash hot path on MI355X.
 
-Headline (BASELINE.json metric, config 2): key hashes/s (device-resident) over
-batched 32-byte keys -- one "step" = one batched launch hashing 16,777,216 keys
-x 32 B (h1 only, as in the metric's 40 B/key algorithmic traffic), inputs already
-resident in HBM.  Two input sets are rotated so the 256 MiB Infinity Cache cannot
-hold the working set.  Multi-GPU (config 4 shape): each rank hashes its own
-contiguous 16M-key shard (weak scaling, no collective inside the timed region);
-with --gather the RCCL gather of the hashes to rank 0 is timed separately.
+Headline (BASELINE.json metric, config 2): key hashes/s (device-resident) over batched
+32-byte keys -- one "step" = one batched launch hashing 16,777,216 keys x 32 B (h1 only,
+40 B/key of algorithmic traffic), inputs already resident in HBM; two input sets are
+rotated so the 256 MiB Infinity Cache cannot hold the working set.
 
-Prints ONE JSON line on rank 0 (contract in the task statement), with the
-dominant kernel's roofline and a CPU baseline (the reference's own hash path,
-oracle/_ref, timed on this host's cores; `port` when that build is absent).
+--gpus N > 1 (config 4: 2^30 x 32 B keys over N GPUs, strong scaling): one process per
+GPU.  Launched by torch.distributed.run (RANK / WORLD_SIZE in the environment) or, when
+those are absent, by this script itself: it starts N fresh child processes before
+touching any GPU and relays rank 0's line.  Each rank hashes its contiguous shard of the
+2^30 keys (no data-path collective: keys are independent, lib/k2hashfunc.cc:49-59); the
+line also times the RCCL gather of every shard's hashes to rank 0 (shard.gather_hashes).
+Every rank's shard is checked against the reference's digests
+(tests/golden/digests.json, fixed32_1G chunks) outside the timed region.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--config fixed32|csr|fixed4096]
+At N = 1 the line also carries secondary results (configs 3, 4 and 5, and the
+host-memory path) and a CPU baseline: the reference's own hash path (oracle/_ref),
+timed on this host's cores.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config fixed32|csr|fixed4096|fixed32_1g|ralledata]
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -28,19 +36,30 @@ ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level parameters)
+# VALU issue roofline: every op of the FNV step (v_xor_b32_sdwa,
+# v_mul_lo_u32, v_lshl_add_u32, v_mad_u64_u32, v_perm_b32) issues at ~4.19 cycles per wave64
+# instruction per SIMD (profiles/r01_valu_rates.txt); 256 CUs x 4 SIMDs at the 2.4 GHz peak.
+VALU_CYCLES_PER_INST = 4.19
+VALU_SIMDS = 1024
+VALU_PEAK_HZ = 2.4e9
+FNV_OPS_PER_CHUNK = 86  # 16 bytes x 5 ops + 2 word pairs x 3 sign-smear ops (k2h_fnv_device.h)
 
+KEYS_1G = 1 << 30
 CONFIGS = {
-    # name: (kind, keys per rank, key_len | (min,max), description)
+    # name: (kind, keys per rank (None: 2^30 / world), key_len | (min,max), description)
     "fixed32": ("fixed", 1 << 24, 32, "16M x 32B fixed-length keys (BASELINE config 2)"),
     "csr": ("csr", 1 << 26, (8, 256), "64M mixed 8-256B keys, offsets+bytes CSR (BASELINE config 3)"),
+    "fixed32_1g": ("fixed", None, 32, "2^30 x 32B keys sharded over the GPUs, RCCL gather of the hashes "
+                                      "(BASELINE config 4)"),
     "fixed4096": ("fixed", 1 << 20, 4096, "1M x 4KiB keys (BASELINE config 5)"),
     # RALLEDATA blobs (hash + subhash + key + value) for a bulk direct set
     "ralledata": ("ralledata", 1 << 23, ((8, 64), (0, 256)),
                   "8M records (keys 8-64B, values 0-256B) -> RALLEDATA blobs with precomputed hashes"),
 }
+METRIC = "key hashes/sec + GiB/s (device-resident), batched 32B keys, 1 MI355X"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=100)
@@ -49,22 +68,97 @@ def parse():
                    help="keep warming up (untimed) until at least this much GPU time has passed: the "
                         "MI355X clock ramps over the first ~30 ms of back-to-back launches "
                         "(tools/clock_ramp.py, profiles/r01_clock_ramp.txt)")
-    p.add_argument("--config", default="fixed32", choices=sorted(CONFIGS))
+    p.add_argument("--config", default=None, choices=sorted(CONFIGS),
+                   help="default: fixed32 at N=1, fixed32_1g (config 4) at N>1")
     p.add_argument("--second", action="store_true", help="also emit the second hash (h2)")
-    p.add_argument("--gather", action="store_true", help="also time the RCCL gather of hashes (N>1)")
     p.add_argument("--index", action="store_true",
                    help="fused bucket-index epilogue (kindex + ckindex outputs, SURVEY 8f rank 1) with a "
                         "2^28-slot table: cur_mask 0x0FFFFFFF, collision_mask 0xF")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--variant", type=int, default=0, help="kernel variant (A/B knob, 0 = auto)")
+    p.add_argument("--no-secondary", action="store_true", help="N=1: skip the secondary configs")
+    p.add_argument("--no-verify", action="store_true", help="skip the digest checks")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
-    return p.parse_args()
+    p.add_argument("--rehearse-cpu", action="store_true",
+                   help="no GPU: run the launcher / shard / gather path on CPU with the scalar plugin "
+                        "(a rehearsal of the N>1 plumbing, not a measurement)")
+    p.add_argument("--keys", type=int, default=0, help="override keys per rank (tests / rehearsals)")
+    p.add_argument("--child-timeout", type=float, default=1500.0)
+    return p.parse_args(argv)
 
 
-def cpu_baseline(keys_host, key_len, n):
-    """Reference hash path on the host cores (rank 0, N=1 only).  Bounded sample:
-    the first `n` keys of the benchmark workload, one pass single-threaded and one
-    pass on `threads` threads."""
+# --------------------------------------------------------------------------------------
+# Launcher: one fresh process per GPU (never an exec of this process)
+# --------------------------------------------------------------------------------------
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args) -> int:
+    """Start args.gpus ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*),
+    relay rank 0's stdout, return the worst exit code.  Runs before anything touches a
+    GPU; the children are new processes."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out, _ = procs[0].communicate(timeout=args.child_timeout)
+    rcs = [procs[0].returncode]
+    for p in procs[1:]:
+        try:
+            rcs.append(p.wait(timeout=60))
+        except subprocess.TimeoutExpired:
+            p.kill()
+            rcs.append(p.wait())
+    sys.stdout.write(out.decode())
+    sys.stdout.flush()
+    return max(abs(rc) for rc in rcs)
+
+
+# --------------------------------------------------------------------------------------
+# Host description and the CPU baseline (rank 0, N = 1)
+# --------------------------------------------------------------------------------------
+def host_info() -> dict:
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+    try:
+        q, per = Path("/sys/fs/cgroup/cpu.max").read_text().split()
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        info["cgroup_cpu_quota"] = None
+    try:
+        txt = Path("/proc/cpuinfo").read_text()
+        names = [ln.split(":", 1)[1].strip() for ln in txt.splitlines() if ln.startswith("model name")]
+        mhz = [float(ln.split(":", 1)[1]) for ln in txt.splitlines() if ln.startswith("cpu MHz")]
+        info["model"] = names[0] if names else None
+        info["mhz_now_avg"] = round(sum(mhz) / len(mhz), 1) if mhz else None
+        mx = Path("/sys/devices/system/cpu/cpu0/cpufreq/cpuinfo_max_freq")
+        info["mhz_max"] = int(mx.read_text()) / 1000 if mx.exists() else None
+    except OSError:
+        pass
+    return info
+
+
+def usable_cores(info: dict) -> int:
+    n = info["affinity"]
+    if info.get("cgroup_cpu_quota"):
+        n = min(n, max(1, int(info["cgroup_cpu_quota"])))
+    omp = os.environ.get("OMP_NUM_THREADS")  # the GPU box's per-GPU CPU share
+    if omp and omp.isdigit():
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(keys_host, key_len: int, n: int) -> dict | None:
+    """Reference hash path on the host cores (rank 0, N=1 only).  Bounded sample: the
+    first n keys of the benchmark workload; best of 3 passes at 1 thread, at the usable
+    cores and at every CPU the OS lists; worker threads are started and parked on a
+    barrier before the clock starts (oracle/cpu_bench.c)."""
     import ctypes
 
     sys.path.insert(0, str(ROOT / "oracle"))
@@ -73,134 +167,104 @@ def cpu_baseline(keys_host, key_len, n):
     lib = oracle.cpubench()
     so = str(oracle.REF_SO) if oracle.REF_SO.exists() else ""
     kind = "reference" if so else "port"
-    threads = int(os.environ.get("K2H_CPU_THREADS", "16"))
+    info = host_info()
+    cores = usable_cores(info)
     ptr = ctypes.c_void_p(keys_host.ctypes.data)
     dig = ctypes.c_uint64()
-    t1 = lib.cpu_bench_fixed(so.encode(), ptr, key_len, n, 1, 1, 0, ctypes.byref(dig))
-    tN = lib.cpu_bench_fixed(so.encode(), ptr, key_len, n, threads, 1, 0, ctypes.byref(dig))
-    # k2hbench `-type rw` hash path, 100k loops (BASELINE config 1)
-    tb = lib.cpu_bench_k2hbench(so.encode(), 100000, 100000, 1, ctypes.byref(dig))
-    if t1 <= 0 or tN <= 0:
+
+    def best(threads, m, inner=8, passes=3):  # seconds per pass over m keys, best of `passes`
+        ts = [lib.cpu_bench_fixed(so.encode(), ptr, key_len, m, threads, inner, 0, ctypes.byref(dig))
+              for _ in range(passes)]
+        return min(ts) / inner if min(ts) > 0 else None
+
+    m1 = min(n, 1 << 22)
+    t1 = best(1, m1)
+    tN = best(cores, n)
+    tall = best(info["nproc"], n) if info["nproc"] and info["nproc"] != cores else tN
+    # k2hbench `-type rw` hash path (BASELINE config 1): 100k loops x 10 scalar calls per
+    # thread on 21-byte "KEY-%016X" keys; per-thread timing like tests/k2hbench.cc:937-976
+    kb1 = min(lib.cpu_bench_k2hbench(so.encode(), 100000, 100000, 1, ctypes.byref(dig)) for _ in range(3))
+    kbN = min(lib.cpu_bench_k2hbench(so.encode(), 100000, 100000, cores, ctypes.byref(dig)) for _ in range(3))
+    if not (t1 and tN):
         return None
     return {
-        "value": n / tN, "unit": "key hashes/s", "cores": threads, "kind": kind,
-        "sample": f"first {n} keys of the same {key_len}B workload, h1 only, one pass on {threads} threads "
-                  f"(reference lib/k2hashfunc.cc k2h_hash via dlsym)",
-        "single_thread": n / t1,
-        "k2hbench_rw_100k": {"seconds": tb, "hash_calls": 1000000, "calls_per_s": 1e6 / tb if tb > 0 else None,
-                              "threads": 1},
+        "value": n / tN, "unit": "key hashes/s", "cores": cores, "kind": kind,
+        "sample": f"first {n} keys of the same {key_len}B workload (first {m1} at 1 thread), h1 only, "
+                  f"8 passes per run, best of 3 runs, on {cores} threads (the box's CPU share; reference "
+                  f"lib/k2hashfunc.cc k2h_hash via dlsym)",
+        "single_thread": m1 / t1,
+        "all_listed_cpus": {"threads": info["nproc"], "value": n / tall if tall else None},
+        "host": info,
+        "k2hbench_rw_100k": {"hash_calls_per_thread": 1000000,
+                              "threads_1": {"seconds": kb1, "calls_per_s": 1e6 / kb1 if kb1 > 0 else None},
+                              f"threads_{cores}": {"seconds": kbN,
+                                                   "calls_per_s": cores * 1e6 / kbN if kbN > 0 else None}},
     }
 
 
-def main():
-    args = parse()
-    import numpy as np
+# --------------------------------------------------------------------------------------
+# Digests of the reference's outputs (tests/golden/digests.json): [xor, wrapping sum,
+# wrapping sum of h*(2i+1)], i = global key index.  Computed on the device.
+# --------------------------------------------------------------------------------------
+def _golden():
+    return json.loads((ROOT / "tests" / "golden" / "digests.json").read_text())["configs"]
+
+
+def digest_dev(h, first: int) -> list[str]:
     import torch
-    import torch.distributed as dist
 
-    import k2hash_amd
-    from k2hash_amd import batch
+    x = h
+    while x.numel() > 1:
+        half = x.numel() // 2
+        y = x[:half] ^ x[half:2 * half]
+        if x.numel() & 1:
+            y[0] ^= x[-1]
+        x = y
+    xr = int(x[0].item()) if x.numel() else 0
+    s = int(h.sum().item())
+    w = 2 * (torch.arange(h.numel(), dtype=torch.int64, device=h.device) + first) + 1
+    ws = int((h * w).sum().item())
+    return [f"{v & (2**64 - 1):016x}" for v in (xr, s, ws)]
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("for --gpus N > 1 launch with torch.distributed.run (one process per GPU)", file=sys.stderr)
-            sys.exit(2)
-    ndev = torch.cuda.device_count()
-    dev = torch.device("cuda", local % max(ndev, 1))  # one process per GPU; wraps only in rehearsals
-    torch.cuda.set_device(dev)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(args.backend)
-    batch.set_variant(args.variant)
 
-    kind, n, shape, desc = CONFIGS[args.config]
-    # --- synthetic input (global key range of this rank), two rotating sets ------------
-    sets = []
-    algo_bytes = 0
-    for s in range(2):
-        first = (s * world + rank) * n
-        if kind == "fixed":
-            keys = batch.synth_bytes(n * shape, dev, byte_off=first * shape)
-            sets.append((keys, None))
-            algo_bytes = n * shape + 8 * n
-        elif kind == "ralledata":
-            (klo, khi), (vlo, vhi) = shape
-            ko = batch.synth_offsets(n, dev, klo, khi, first_key=first)
-            vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7, first_key=first)
-            kb, vb = int(ko[-1].item()), int(vo[-1].item())
-            kd = batch.synth_bytes(kb, dev, byte_off=s * (1 << 36) + rank * (1 << 34))
-            vd = batch.synth_bytes(vb, dev, byte_off=s * (1 << 36) + rank * (1 << 34) + (1 << 33))
-            blob = torch.empty(80 * n + kb + vb, dtype=torch.uint8, device=dev)
-            boff = torch.empty(n + 1, dtype=torch.int64, device=dev)
-            sets.append(((kd, ko, vd, vo), (blob, boff)))
-            # minimal traffic: key + value bytes and their offsets in, blobs + blob offsets out
-            algo_bytes = max(algo_bytes, (kb + vb + 16 * (n + 1)) + (80 * n + kb + vb + 8 * (n + 1)))
-        else:
-            off = batch.synth_offsets(n, dev, shape[0], shape[1], first_key=first)
-            data = batch.synth_bytes(int(off[-1].item()), dev, byte_off=s * (1 << 36) + rank * (1 << 34))
-            sets.append((data, off))
-            algo_bytes = max(algo_bytes, int(off[-1].item()) + 8 * n + 8 * (n + 1))
-    if args.second:
-        algo_bytes += 8 * n
-    if args.index:
-        algo_bytes += 16 * n  # kindex + ckindex writes
-    outs = [(torch.empty(n, dtype=torch.int64, device=dev),
-             torch.empty(n, dtype=torch.int64, device=dev) if args.second else None) for _ in range(2)]
-    idx = [(torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
-           for _ in range(2)] if args.index else None
-    torch.cuda.synchronize()
-    lib = k2hash_amd._native.batch_lib()
-    CUR_MASK, CMASK = (1 << 28) - 1, 0xF
+def verify_chunks(h, first: int, chunks) -> dict:
+    """Check every reference chunk that lies wholly inside [first, first + h.numel())."""
+    ok, checked = True, 0
+    for c in chunks:
+        a, b = c["first"], c["first"] + c["count"]
+        if a >= first and b <= first + h.numel():
+            ok &= digest_dev(h[a - first:b - first], a) == c["h1"]
+            checked += 1
+    return {"chunks_checked": checked, "ok": bool(ok)}
 
-    def step(i):
-        keys, off = sets[i & 1]
-        if kind == "ralledata":
-            from k2hash_amd import ralledata
-            (kd, ko, vd, vo), (blob, boff) = keys, off
-            ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff, total=blob.numel())
-            return
-        if args.index:
-            import ctypes
-            h1, h2 = outs[i & 1]
-            k, c = idx[i & 1]
-            p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-            s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
-            if kind == "fixed":
-                rc = lib.k2h_amd_hash_fixed_index(p(keys), shape, n, p(h1), p(h2), 0, CUR_MASK, CMASK, p(k), p(c), s)
-            else:
-                rc = lib.k2h_amd_hash_csr_index(p(keys), p(off), n, p(h1), p(h2), 0, CUR_MASK, CMASK, p(k), p(c), s)
-            k2hash_amd._native.check(rc)
-        elif kind == "fixed":
-            k2hash_amd.hash_fixed(keys, shape, second=args.second, out=outs[i & 1])
-        else:
-            k2hash_amd.hash_csr(keys, off, second=args.second, out=outs[i & 1])
 
-    for i in range(args.warmup):
+# --------------------------------------------------------------------------------------
+# Timing
+# --------------------------------------------------------------------------------------
+def timed(step, steps: int, warmup: int, warm_ms: float, world: int = 1, dist=None, dev=None):
+    """W untimed launches, then warm up for >= warm_ms, then EXACTLY `steps` launches bracketed
+    by barrier + synchronize.  Returns (wall seconds (max over ranks), average launch time from
+    one event pair on the launch stream, extra warm-up launches)."""
+    import torch
+
+    for i in range(warmup):
         step(i)
     torch.cuda.synchronize()
-    w0 = time.perf_counter()
-    extra = 0
-    while (time.perf_counter() - w0) * 1e3 < args.warm_ms:
-        for i in range(20):
+    w0, extra = time.perf_counter(), 0
+    while (time.perf_counter() - w0) * 1e3 < warm_ms:
+        for i in range(10):
             step(i)
-        extra += 20
+        extra += 10
         torch.cuda.synchronize()
-    # One event pair around the K back-to-back launches on the stream they run on:
-    # kernel time per launch = (end - start) / K (inter-kernel gaps included, ~1-2 us).
-    e_start, e_end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    e_start.record()
-    for i in range(args.steps):
+    e0.record()
+    for i in range(steps):
         step(i)
-    e_end.record()
+    e1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
@@ -210,43 +274,346 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    kern_avg_s = e_start.elapsed_time(e_end) / args.steps / 1e3
+    return elapsed, e0.elapsed_time(e1) / steps / 1e3, extra
+
+
+def valu_fields(name: str, kern_s: float, model_insts: float) -> dict:
+    """VALU-issue roofline: wave64 VALU instructions per launch (rocprofv3 SQ_INSTS_VALU pass,
+    profiles/valu_<name>.json, else the FNV-step model) at the peak issue rate, over the
+    measured launch time."""
+    insts, src = model_insts, "model: 86 slow-issue VALU ops per 16-byte chunk per 64 keys"
+    prof = ROOT / "profiles" / f"valu_{name}.json"
+    if prof.exists():
+        d = json.loads(prof.read_text())
+        insts, src = float(d["valu_insts_per_launch"]), f"profiles/valu_{name}.json ({d.get('round', '')})"
+    floor_s = insts * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_PEAK_HZ)
+    return {"valu_frac": floor_s / kern_s, "valu_insts_per_launch": insts, "valu_floor_us": floor_s * 1e6,
+            "valu_source": src}
+
+
+def traffic_of(name: str):
+    prof = ROOT / "profiles" / f"traffic_{name}.json"
+    return json.loads(prof.read_text()).get("hbm_bytes_per_launch") if prof.exists() else None
+
+
+def roofline(name: str, algo_bytes: int, kern_s: float, model_insts: float) -> dict:
+    achieved = algo_bytes / kern_s / 1e9
+    r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_of(name), "algorithmic_bytes_per_launch": algo_bytes}
+    r.update(valu_fields(name, kern_s, model_insts))
+    return r
+
+
+def chunks_of(length: int) -> int:
+    return (length + 15) // 16
+
+
+# --------------------------------------------------------------------------------------
+# Secondary results at N = 1 (configs 3, 4, 5 and the host-memory path)
+# --------------------------------------------------------------------------------------
+def secondary_csr(dev, steps, warm_ms, verify):
+    import torch
+
+    import k2hash_amd
+    from k2hash_amd import batch
+
+    n, (lo, hi) = CONFIGS["csr"][1], CONFIGS["csr"][2]
+    off = batch.synth_offsets(n, dev, lo, hi)
+    nbytes = int(off[-1].item())
+    data = batch.synth_bytes(nbytes, dev)
+    h1 = torch.empty(n, dtype=torch.int64, device=dev)
+    wall, kern, _ = timed(lambda i: k2hash_amd.hash_csr(data, off, out=(h1, None)), steps, 3, warm_ms)
+    algo = nbytes + 8 * n + 8 * (n + 1)
+    model = sum(chunks_of(L) for L in range(lo, hi + 1)) / (hi - lo + 1) * FNV_OPS_PER_CHUNK * n / 64
+    res = {"workload": CONFIGS["csr"][3], "keys": n, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
+           "value": n * steps / wall, "unit": "key hashes/s", "roofline": roofline("csr", algo, kern, model)}
+    if verify:
+        res["verify"] = verify_chunks(h1, 0, _golden()["csr_8_256_64M"]["chunks"])
+    del off, data, h1
+    torch.cuda.empty_cache()
+    return res
+
+
+def secondary_fixed(name, dev, steps, warm_ms, verify, golden_name):
+    import torch
+
+    import k2hash_amd
+    from k2hash_amd import batch
+
+    _, n, L, desc = CONFIGS[name]
+    n = n or KEYS_1G
+    keys = batch.synth_bytes(n * L, dev)
+    h1 = torch.empty(n, dtype=torch.int64, device=dev)
+    wall, kern, _ = timed(lambda i: k2hash_amd.hash_fixed(keys, L, out=(h1, None)), steps, 3, warm_ms)
+    algo = n * L + 8 * n
+    model = n / 64 * chunks_of(L) * FNV_OPS_PER_CHUNK
+    res = {"workload": desc + (" -- all 2^30 keys on one GPU" if name == "fixed32_1g" else ""), "keys": n,
+           "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3, "value": n * steps / wall,
+           "unit": "key hashes/s", "key_gib_per_s": n * L * steps / wall / 2**30,
+           "roofline": roofline(name, algo, kern, model)}
+    if verify:
+        g = _golden()[golden_name]
+        res["verify"] = verify_chunks(h1, 0, g.get("chunks") or [dict(first=0, count=g["n"], h1=g["h1"])])
+    del keys, h1
+    torch.cuda.empty_cache()
+    return res
+
+
+def secondary_host(dev, reps=5):
+    """Host-memory path (PCIe-inclusive; never `value`): 16M x 32 B keys in pageable host
+    memory -> k2h_amd_hash_fixed_host -> hashes in host memory."""
+    import numpy as np
+
+    import k2hash_amd
+    from k2hash_amd import batch
+
+    n, L = CONFIGS["fixed32"][1], 32
+    keys = batch.synth_bytes(n * L, dev).cpu().numpy()
+    h1 = None
+    ts = []
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        h1, _ = k2hash_amd.hash_fixed_host(keys, L)
+        t = time.perf_counter() - t0
+        if r:
+            ts.append(t)
+    t = min(ts)
+    moved = n * L + 8 * n
+    g = _golden()["fixed32_16M"]
+    ok = None
+    try:
+        import torch
+
+        ok = digest_dev(torch.from_numpy(h1.view(np.int64)), 0) == g["h1"]
+    except Exception:  # noqa: BLE001 -- verification is best effort here
+        ok = None
+    return {"workload": "16M x 32B keys, pageable host memory in and out (k2h_amd_hash_fixed_host)", "keys": n,
+            "ms_per_call_best": t * 1e3, "ms_per_call_median": sorted(ts)[len(ts) // 2] * 1e3,
+            "value": n / t, "unit": "key hashes/s", "moved_gb_per_s": moved / t / 1e9, "verify_ok": ok}
+
+
+# --------------------------------------------------------------------------------------
+# Rehearsal of the N > 1 plumbing without a GPU (scalar plugin hashes, gloo gather)
+# --------------------------------------------------------------------------------------
+def rehearse_cpu(args, world, rank):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import k2hash_amd
+    from k2hash_amd import shard
+
+    dist.init_process_group(args.backend if args.backend != "nccl" else "gloo")
+    total = args.keys or 4096
+    first, last = shard.shard_range(total, rank, world)
+    raw = np.random.default_rng(1234).integers(0, 256, size=total * 32, dtype=np.uint8)[first * 32:last * 32]
+    h = None
+
+    def step(_):
+        nonlocal h
+        h = torch.tensor([k2hash_amd.k2h_hash(raw[i * 32:(i + 1) * 32].tobytes()) for i in range(last - first)],
+                         dtype=torch.uint64).view(torch.int64)
+
+    for i in range(args.warmup):
+        step(i)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    out = shard.gather_hashes(h, counts=shard.shard_counts(total, world))
+    if rank == 0:
+        ref = [k2hash_amd.k2h_hash(np.random.default_rng(1234).integers(0, 256, size=total * 32, dtype=np.uint8)
+                                   [i * 32:(i + 1) * 32].tobytes()) for i in range(total)]
+        ok = out.view(torch.uint64).tolist() == ref
+        print(json.dumps({"metric": METRIC, "value": total * args.steps / float(el.item()), "unit": "key hashes/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ms_per_step": float(el.item()) / args.steps * 1e3, "higher_is_better": True,
+                          "scaling": "strong", "vs_baseline": None, "dtype": "u64 (u8 key bytes in)",
+                          "data": "synthetic", "device": "cpu rehearsal (scalar plugin; NOT a measurement)",
+                          "config": {"workload": f"{total} x 32B keys sharded over {world} ranks",
+                                     "parallelism": f"shard{world}"},
+                          "gather": {"ok": ok, "backend": dist.get_backend()}}), flush=True)
+    dist.destroy_process_group()
+
+
+# --------------------------------------------------------------------------------------
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch(args))  # before anything touches a GPU
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_cpu:
+        return rehearse_cpu(args, world, rank)
+
+    import torch
+    import torch.distributed as dist
+
+    import k2hash_amd
+    from k2hash_amd import batch, shard
+
+    name = args.config or ("fixed32" if world == 1 else "fixed32_1g")
+    kind, n, shape, desc = CONFIGS[name]
+    ndev = torch.cuda.device_count()
+    dev = torch.device("cuda", local % max(ndev, 1))  # one process per GPU; wraps only in rehearsals
+    torch.cuda.set_device(dev)
+    if world > 1:
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
+
+    # --- synthetic input: this rank's global key range -----------------------------------
+    strong = n is None
+    if strong:
+        first, last = shard.shard_range(KEYS_1G, rank, world)
+        n = last - first
+    else:
+        first = rank * n
+    if args.keys:
+        n = args.keys
+    nsets = 1 if strong else 2  # config 4's shards (>= 4 GiB) dwarf the 256 MiB Infinity Cache
+    sets, algo_bytes, key_bytes = [], 0, 0
+    for s in range(nsets):
+        base = first + s * world * n  # set 0 is the rank's shard of the reference workload
+        if kind == "fixed":
+            sets.append((batch.synth_bytes(n * shape, dev, byte_off=base * shape), None))
+            algo_bytes, key_bytes = n * shape + 8 * n, n * shape
+        elif kind == "ralledata":
+            (klo, khi), (vlo, vhi) = shape
+            ko = batch.synth_offsets(n, dev, klo, khi, first_key=base)
+            vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7, first_key=base)
+            kb, vb = int(ko[-1].item()), int(vo[-1].item())
+            kd = batch.synth_bytes(kb, dev, byte_off=s * (1 << 36) + rank * (1 << 34))
+            vd = batch.synth_bytes(vb, dev, byte_off=s * (1 << 36) + rank * (1 << 34) + (1 << 33))
+            blob = torch.empty(80 * n + kb + vb, dtype=torch.uint8, device=dev)
+            boff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+            sets.append(((kd, ko, vd, vo), (blob, boff)))
+            # minimal traffic: key + value bytes and their offsets in, blobs + blob offsets out
+            algo_bytes = max(algo_bytes, (kb + vb + 16 * (n + 1)) + (80 * n + kb + vb + 8 * (n + 1)))
+            key_bytes = max(key_bytes, kb)
+        else:
+            off = batch.synth_offsets(n, dev, shape[0], shape[1], first_key=base)
+            nb = int(off[-1].item())
+            data = batch.synth_bytes(nb, dev, byte_off=s * (1 << 36) + rank * (1 << 34))
+            sets.append((data, off))
+            algo_bytes, key_bytes = max(algo_bytes, nb + 8 * n + 8 * (n + 1)), max(key_bytes, nb)
+    if args.second:
+        algo_bytes += 8 * n
+    if args.index:
+        algo_bytes += 16 * n  # kindex + ckindex writes
+    outs = [(torch.empty(n, dtype=torch.int64, device=dev),
+             torch.empty(n, dtype=torch.int64, device=dev) if args.second else None) for _ in range(nsets)]
+    idx = [(torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
+           for _ in range(nsets)] if args.index else None
+    torch.cuda.synchronize()
+    CUR_MASK, CMASK = (1 << 28) - 1, 0xF
+
+    def step(i):
+        keys, off = sets[i % nsets]
+        if kind == "ralledata":
+            from k2hash_amd import ralledata
+            (kd, ko, vd, vo), (blob, boff) = keys, off
+            ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff, total=blob.numel())
+        elif args.index:
+            h1, h2 = outs[i % nsets]
+            k, c = idx[i % nsets]
+            if kind == "fixed":
+                batch.hash_fixed_index(keys, shape, CUR_MASK, CMASK, second=args.second, out=(h1, h2, k, c))
+            else:
+                batch.hash_csr_index(keys, off, CUR_MASK, CMASK, second=args.second, out=(h1, h2, k, c))
+        elif kind == "fixed":
+            k2hash_amd.hash_fixed(keys, shape, second=args.second, out=outs[i % nsets])
+        else:
+            k2hash_amd.hash_csr(keys, off, second=args.second, out=outs[i % nsets])
+
+    elapsed, kern_s, extra = timed(step, args.steps, args.warmup, args.warm_ms, world, dist, dev)
     total_keys = n * world * args.steps
     value = total_keys / elapsed
 
+    # --- verification against the reference's digests (outside the timed region) ---------
+    verify = None
+    if not args.no_verify and kind == "fixed" and not args.keys:
+        gname = {"fixed32": "fixed32_16M", "fixed32_1g": "fixed32_1G", "fixed4096": "fixed4096_1M"}[name]
+        g = _golden()[gname]
+        if name == "fixed32":  # set 0 of rank 0 is exactly the reference's 16M-key workload
+            verify = {"ok": rank != 0 or digest_dev(outs[0][0], 0) == g["h1"], "chunks_checked": 1}
+        else:
+            verify = verify_chunks(outs[0][0], first, g.get("chunks") or [dict(first=0, count=g["n"], h1=g["h1"])])
+        if world > 1:
+            t = torch.tensor([0 if verify["ok"] else 1, verify["chunks_checked"]], dtype=torch.int64, device=dev)
+            dist.all_reduce(t)
+            verify = {"ok": int(t[0].item()) == 0, "chunks_checked": int(t[1].item()), "ranks": world}
+
+    # --- config 4: the RCCL gather of every shard's hashes to rank 0 ------------------------
     gather = None
-    if args.gather and world > 1:
-        from k2hash_amd.shard import gather_hashes
+    if world > 1:
+        counts = shard.shard_counts(KEYS_1G, world) if strong and not args.keys else [n] * world
         h = outs[0][0]
+        gsteps = max(3, min(10, args.steps // 10))
+        res = None
         for _ in range(2):
-            gather_hashes(h)
+            res = shard.gather_hashes(h, counts=counts)
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
-        for _ in range(5):
-            gather_hashes(h)
+        for _ in range(gsteps):
+            res = shard.gather_hashes(h, counts=counts)
         torch.cuda.synchronize()
         dist.barrier()
-        gather = {"ms_per_gather": (time.perf_counter() - g0) / 5 * 1e3,
-                  "bytes_to_root": 8 * n * (world - 1)}
+        gs = torch.tensor([(time.perf_counter() - g0) / gsteps], dtype=torch.float64, device=dev)
+        dist.all_reduce(gs, op=dist.ReduceOp.MAX)
+        gather_s = float(gs.item())
+        # hash + gather back to back (the end-to-end step of a bulk loader)
+        dist.barrier()
+        torch.cuda.synchronize()
+        c0 = time.perf_counter()
+        for i in range(gsteps):
+            step(0)
+            res = shard.gather_hashes(h, counts=counts)
+        torch.cuda.synchronize()
+        dist.barrier()
+        cs = torch.tensor([(time.perf_counter() - c0) / gsteps], dtype=torch.float64, device=dev)
+        dist.all_reduce(cs, op=dist.ReduceOp.MAX)
+        combo_s = float(cs.item())
+        gok = None
+        if rank == 0 and not args.no_verify and strong and not args.keys:
+            gok = verify_chunks(res, 0, _golden()["fixed32_1G"]["chunks"])
+        gather = {"backend": dist.get_backend(), "ms_per_gather": gather_s * 1e3,
+                  "bytes_to_root": 8 * (sum(counts) - counts[0]),
+                  "root_recv_gb_per_s": 8 * (sum(counts) - counts[0]) / gather_s / 1e9,
+                  "with_gather": {"ms_per_step": combo_s * 1e3, "value": sum(counts) / combo_s,
+                                  "unit": "key hashes/s (hashed and gathered at rank 0)"},
+                  "verify_root": gok}
+        del res
 
+    secondary = None
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and kind == "fixed":
-        m = n if shape <= 64 else max(1, (512 << 20) // shape)
-        host = sets[0][0][: m * shape].cpu().numpy()
-        cpu = cpu_baseline(host, shape, m)
+    if rank == 0 and world == 1 and name == "fixed32" and not (args.index or args.second or args.keys):
+        if not args.no_secondary:
+            del sets, outs
+            torch.cuda.empty_cache()
+            vf = not args.no_verify
+            secondary = {
+                "csr": secondary_csr(dev, 20, 60.0, vf),
+                "fixed4096": secondary_fixed("fixed4096", dev, 20, 60.0, vf, "fixed4096_1M"),
+                "fixed32_1g": secondary_fixed("fixed32_1g", dev, 10, 60.0, vf, "fixed32_1G"),
+                "host_fixed32": secondary_host(dev),
+            }
+        if not args.no_cpu_baseline:
+            host = batch.synth_bytes(n * shape, dev).cpu().numpy()
+            cpu = cpu_baseline(host, shape, n)
 
     if rank == 0:
-        achieved = algo_bytes / kern_avg_s / 1e9
-        traffic = None
-        prof = ROOT / "profiles" / f"traffic_{args.config}{'_index' if args.index else ''}{'_h2' if args.second else ''}.json"
-        if prof.exists():
-            traffic = json.loads(prof.read_text()).get("hbm_bytes_per_launch")
-        key_bytes = n * (shape if kind == "fixed" else (shape[0][0] + shape[0][1]) / 2 if kind == "ralledata"
-                         else (shape[0] + shape[1]) / 2)
+        model = (n / 64 * chunks_of(shape) * FNV_OPS_PER_CHUNK if kind == "fixed"
+                 else key_bytes / 16 * FNV_OPS_PER_CHUNK / 64)
+        prof_name = f"{name}{'_index' if args.index else ''}{'_h2' if args.second else ''}"
         line = {
-            "metric": "key hashes/sec + GiB/s (device-resident), batched 32B keys, 1 MI355X"
-            if args.config == "fixed32" and not (args.index or args.second)
+            "metric": METRIC if kind == "fixed" and shape == 32 and not (args.index or args.second)
             else f"RALLEDATA records/sec (device-resident), {desc}" if kind == "ralledata"
             else f"key hashes{' + bucket indices' if args.index else ''}/sec (device-resident), {desc}",
             "value": value,
@@ -257,24 +624,24 @@ def main():
             "warmup_extra_for_clock_ramp": extra,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "u64 (u8 key bytes in)",
             "data": "synthetic (splitmix64 counter stream, generated on device; SURVEY.md 8d spec in DESIGN.md)",
-            "config": {"workload": desc, "keys_per_gpu": n,
+            "config": {"workload": desc, "keys_per_gpu": n, "keys_total": n * world,
                        "key_len": shape if kind == "fixed" else list(shape),
                        "second_hash": bool(args.second), "bucket_index": bool(args.index),
-                       "parallelism": f"shard{world}",
-                       "variant": args.variant},
+                       "parallelism": f"shard{world}"},
             "key_gib_per_s": value * (key_bytes / n) / 2**30,
-            "kernel_ms": kern_avg_s * 1e3,
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
-                         "algorithmic_bytes_per_launch": algo_bytes},
+            "kernel_ms": kern_s * 1e3,
+            "roofline": roofline(prof_name, algo_bytes, kern_s, model),
+            "verify": verify,
             "cpu_baseline": cpu,
         }
         if gather:
             line["gather"] = gather
+        if secondary:
+            line["secondary"] = secondary
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -238,8 +238,6 @@ int k2h_amd_import_scan_prehash_device(const void* file, uint64_t size, int form
 /* Identity / diagnostics. */
 const char* k2h_amd_version(void);     /* library + kernel identity, e.g. "k2hash_amd 0.1 gfx950" */
 const char* k2h_amd_strerror(int code); /* message for `code`, with the last HIP error if any */
-int k2h_amd_set_variant(int variant);   /* A/B knob for measurement; 0 = auto (default) */
-int k2h_amd_get_variant(void);
 
 /* Synthetic-workload generator used by bench.py and the tests (not the hash
  * path): writes bytes [byte_off, byte_off+nbytes) of the splitmix64 word stream

@@ -129,16 +129,20 @@ def bucket_index(h1, cur_mask: int, collision_mask: int, kindex: bool = True, ck
 
 
 def hash_fixed_index(keys, key_len: int, cur_mask: int, collision_mask: int, second: bool = False,
-                     std_fnv: bool = False, kindex: bool = True, ckindex: bool = True, stream=None):
-    """hash_fixed + bucket index in one pass: returns (h1, h2, kindex, ckindex)."""
+                     std_fnv: bool = False, kindex: bool = True, ckindex: bool = True, stream=None, out=None):
+    """hash_fixed + bucket index in one pass: returns (h1, h2, kindex, ckindex).  `out`:
+    preallocated (h1, h2, kindex, ckindex) tensors (h2 / kindex / ckindex may be None)."""
     torch = _torch()
     _check_dev(keys, "keys", torch.uint8)
     if key_len <= 0:
         raise ValueError("key_len must be positive")
     n = keys.numel() // key_len
-    h1 = torch.empty(n, dtype=torch.int64, device=keys.device)
-    h2 = torch.empty(n, dtype=torch.int64, device=keys.device) if second else None
-    k, c = _index_outs(torch, n, keys.device, kindex, ckindex, None)
+    if out is not None:
+        h1, h2, k, c = out
+    else:
+        h1 = torch.empty(n, dtype=torch.int64, device=keys.device)
+        h2 = torch.empty(n, dtype=torch.int64, device=keys.device) if second else None
+        k, c = _index_outs(torch, n, keys.device, kindex, ckindex, None)
     rc = _native.batch_lib().k2h_amd_hash_fixed_index(
         _dev_ptr(keys), key_len, n, _dev_ptr(h1), _dev_ptr(h2) if h2 is not None else None,
         FLAG_STD_FNV if std_fnv else 0, cur_mask, collision_mask, _dev_ptr(k) if k is not None else None,
@@ -148,7 +152,7 @@ def hash_fixed_index(keys, key_len: int, cur_mask: int, collision_mask: int, sec
 
 
 def hash_csr_index(data, offsets, cur_mask: int, collision_mask: int, second: bool = False,
-                   std_fnv: bool = False, kindex: bool = True, ckindex: bool = True, stream=None):
+                   std_fnv: bool = False, kindex: bool = True, ckindex: bool = True, stream=None, out=None):
     """hash_csr + bucket index in one pass: returns (h1, h2, kindex, ckindex)."""
     torch = _torch()
     _check_dev(data, "data", torch.uint8)
@@ -156,9 +160,12 @@ def hash_csr_index(data, offsets, cur_mask: int, collision_mask: int, second: bo
     n = offsets.numel() - 1
     if n < 0:
         raise ValueError("offsets must have n+1 entries")
-    h1 = torch.empty(n, dtype=torch.int64, device=data.device)
-    h2 = torch.empty(n, dtype=torch.int64, device=data.device) if second else None
-    k, c = _index_outs(torch, n, data.device, kindex, ckindex, None)
+    if out is not None:
+        h1, h2, k, c = out
+    else:
+        h1 = torch.empty(n, dtype=torch.int64, device=data.device)
+        h2 = torch.empty(n, dtype=torch.int64, device=data.device) if second else None
+        k, c = _index_outs(torch, n, data.device, kindex, ckindex, None)
     base = _dev_ptr(data) if data.numel() > 0 else ctypes.c_void_p(data.data_ptr() or 1)
     rc = _native.batch_lib().k2h_amd_hash_csr_index(
         base, _dev_ptr(offsets), n, _dev_ptr(h1), _dev_ptr(h2) if h2 is not None else None,
@@ -229,14 +236,6 @@ def synth_offsets(n: int, device, min_len: int = 8, max_len: int = 256, seed: in
     off = torch.zeros(n + 1, dtype=torch.int64, device=device)
     torch.cumsum(lens, dim=0, dtype=torch.int64, out=off[1:])
     return off
-
-
-def set_variant(v: int) -> int:
-    return _native.batch_lib().k2h_amd_set_variant(v)
-
-
-def get_variant() -> int:
-    return _native.batch_lib().k2h_amd_get_variant()
 
 
 def version() -> str:

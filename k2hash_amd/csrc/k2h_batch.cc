@@ -27,15 +27,23 @@
 namespace {
 
 thread_local char g_err[256];
-int g_variant = -1;  // -1: read K2H_AMD_VARIANT once
 
+#if K2H_AMD_LAB
+// Measurement lab only (tools/lab): a process-global kernel-variant knob for A/B runs.
+std::atomic<int> g_variant{-1};  // -1: read K2H_AMD_VARIANT once
 int variant() {
-  if (g_variant < 0) {
-    const char* v = getenv("K2H_AMD_VARIANT");
-    g_variant = v ? atoi(v) : 0;
+  int v = g_variant.load(std::memory_order_relaxed);
+  if (v < 0) {
+    const char* e = getenv("K2H_AMD_VARIANT");
+    int want = e ? atoi(e) : 0;
+    g_variant.compare_exchange_strong(v, want);
+    v = g_variant.load(std::memory_order_relaxed);
   }
-  return g_variant;
+  return v;
 }
+#else
+constexpr int variant() { return k2h::kVariantAuto; }  // the product runs the default kernels
+#endif
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
   if (e != hipSuccess)
@@ -211,17 +219,53 @@ int slot_drain(Slot& s, uint64_t* h1, uint64_t* h2) {
   return K2H_AMD_OK;
 }
 
+// Forget a slot's pending chunk without copying it anywhere: waits for the device work that
+// still writes into the slot's buffers.  Every host call starts by discarding both slots,
+// and every error return discards them too, so a chunk left behind by a failed call can
+// never be drained into a later caller's output.
+void slot_discard(Slot& s) {
+  if (s.busy && s.done) (void)hipEventSynchronize(s.done);
+  s.busy = false;
+}
+
+struct SlotsGuard {  // discards both slots on entry and on every return path
+  HostCtx& c;
+  explicit SlotsGuard(HostCtx& ctx) : c(ctx) {
+    slot_discard(c.slot[0]);
+    slot_discard(c.slot[1]);
+  }
+  ~SlotsGuard() {
+    slot_discard(c.slot[0]);
+    slot_discard(c.slot[1]);
+  }
+};
+
 constexpr uint64_t kChunkBytes = 64ull << 20;  // 64 MiB of key bytes per pipeline chunk
 constexpr uint64_t kChunkKeysMax = 4ull << 20;
 
-int set_device(int device) {
-  int count = 0;
-  hipError_t e = hipGetDeviceCount(&count);
-  if (e != hipSuccess || count == 0) return fail(K2H_AMD_ENODEV, "no HIP device", e);
-  if (device < 0 || device >= count || device >= 64) return fail(K2H_AMD_EINVAL, "device index out of range");
-  if ((e = hipSetDevice(device)) != hipSuccess) return fail(K2H_AMD_EHIP, "hipSetDevice", e);
-  return K2H_AMD_OK;
-}
+// Makes `device` current for the duration of a host-pointer call and restores the caller's
+// current device on every return path (a torch process must not see its current
+// device change under it).
+class DeviceGuard {
+ public:
+  int enter(int device) {
+    int count = 0;
+    hipError_t e = hipGetDeviceCount(&count);
+    if (e != hipSuccess || count == 0) return fail(K2H_AMD_ENODEV, "no HIP device", e);
+    if (device < 0 || device >= count || device >= 64) return fail(K2H_AMD_EINVAL, "device index out of range");
+    if ((e = hipGetDevice(&prev_)) != hipSuccess) return fail(K2H_AMD_EHIP, "hipGetDevice", e);
+    if (prev_ != device && (e = hipSetDevice(device)) != hipSuccess) return fail(K2H_AMD_EHIP, "hipSetDevice", e);
+    set_ = prev_ != device;
+    return K2H_AMD_OK;
+  }
+  ~DeviceGuard() {
+    if (set_) (void)hipSetDevice(prev_);
+  }
+
+ private:
+  int prev_ = -1;
+  bool set_ = false;
+};
 
 }  // namespace
 
@@ -323,10 +367,12 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed_host(const void* k
     if (h2) memset(h2, 0, n * 8);
     return K2H_AMD_OK;
   }
-  int rc = set_device(device);
+  DeviceGuard dg;
+  int rc = dg.enter(device);
   if (rc) return rc;
   HostCtx& c = g_ctx[device];
   std::lock_guard<std::mutex> lk(c.mu);
+  SlotsGuard sg(c);
   uint64_t per = kChunkBytes / key_len;
   if (per == 0) per = 1;
   if (per > kChunkKeysMax) per = kChunkKeysMax;
@@ -367,10 +413,12 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* byt
   }
   for (uint64_t i = 0; i < n; ++i)
     if (offsets[i + 1] < offsets[i]) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
-  int rc = set_device(device);
+  DeviceGuard dg;
+  int rc = dg.enter(device);
   if (rc) return rc;
   HostCtx& c = g_ctx[device];
   std::lock_guard<std::mutex> lk(c.mu);
+  SlotsGuard sg(c);
   const uint8_t* src = (const uint8_t*)bytes;
   int k = 0;
   uint64_t first = 0;
@@ -502,7 +550,8 @@ __attribute__((visibility("default"))) int k2h_amd_build_ralledata_host(
       if (off[s][i + 1] < off[s][i]) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
     total += off[s][n] - off[s][0];
   }
-  int rc = set_device(device);
+  DeviceGuard dg;
+  int rc = dg.enter(device);
   if (rc) return rc;
   hipStream_t st;
   hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
@@ -553,13 +602,10 @@ __attribute__((visibility("default"))) const char* k2h_amd_strerror(int code) {
   return "unknown error";
 }
 
-__attribute__((visibility("default"))) int k2h_amd_set_variant(int v) {
-  int old = variant();
-  g_variant = v;
-  return old;
-}
-
+#if K2H_AMD_LAB
+__attribute__((visibility("default"))) int k2h_amd_set_variant(int v) { return g_variant.exchange(v); }
 __attribute__((visibility("default"))) int k2h_amd_get_variant(void) { return variant(); }
+#endif
 
 __attribute__((visibility("default"))) int k2h_amd_synth_bytes(void* out, uint64_t nbytes, uint64_t seed,
                                                                uint64_t byte_off, void* stream) {

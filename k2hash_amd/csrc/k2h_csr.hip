@@ -93,7 +93,7 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) {
     uint32_t o = (uint32_t)__shfl_xor((int)v, d, 64);
@@ -1091,7 +1091,8 @@ static hipError_t launch_lean2(const uint8_t* b, const uint64_t* offsets, uint64
   return hipGetLastError();
 }
 
-hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+#if K2H_AMD_LAB
+static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
   SpadTable t = make_spad(seed);
   unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
@@ -1180,12 +1181,38 @@ hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t 
   if (bp) return launch_bucket_index(h1, n, *bp, stream);  // A/B modes: unfused epilogue
   return hipGetLastError();
 }
+#endif  // K2H_AMD_LAB
+
+static_assert(kCsrDefaultMode == kModeLean2Ring, "product CSR mode");
+
+hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+                           uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
+#if K2H_AMD_LAB
+  if (mode != kModeLean2Ring) return launch_csr_tile_lab(bytes, offsets, n, seed, h1, h2, mode, stream, bp);
+#else
+  (void)mode;
+#endif
+  // 512-key tiles staged by the lean2 kernel (pair walk); tiles whose bytes exceed its
+  // 72 KiB stage are listed and hashed by the line-ring kernel in a second launch on the
+  // same stream (none for BASELINE config 3).
+  const SpadTable t = make_spad(seed);
+  const unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
+  uint32_t* scratch = nullptr;  // [0] = count, [1..] = tile list
+  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (g + 1), stream);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(scratch, 0, 4, stream);
+  const unsigned gl = g < 512u ? g : 512u;  // ring kernel: ~78 KiB LDS, two blocks per CU
+  if (e == hipSuccess) e = launch_lean2<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, scratch, g, gl, bp, stream);
+  hipError_t f = hipFreeAsync(scratch, stream);
+  return e != hipSuccess ? e : f;
+}
 
 bool fixed_lines_ok(const void* keys, uint64_t key_len) {
   return key_len >= 128 && (key_len & 127u) == 0 && ((uintptr_t)keys & 127u) == 0 && key_len < (1ull << 26);
 }
 
-hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
+#if K2H_AMD_LAB
+static hipError_t launch_fixed_long_lab(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
                              uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
   const uint8_t* k = (const uint8_t*)keys;
   if (mode == kLongAuto) mode = fixed_lines_ok(keys, key_len) ? kLongLines2 : kLongRing;
@@ -1249,6 +1276,50 @@ hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uin
     else fnv_fixed_long_kernel<false, false><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr);
   }
   if (bp) return launch_bucket_index(h1, n, *bp, stream);
+  return hipGetLastError();
+}
+#endif  // K2H_AMD_LAB
+
+hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
+                             uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
+#if K2H_AMD_LAB
+  if (mode > kLongLines2) return launch_fixed_long_lab(keys, key_len, n, seed, h1, h2, mode, stream, bp);
+#endif
+  const uint8_t* k = (const uint8_t*)keys;
+  if (mode == kLongAuto) mode = fixed_lines_ok(keys, key_len) ? kLongLines2 : kLongRing;
+  if (mode == kLongLines2 && !fixed_lines_ok(keys, key_len)) mode = kLongRing;
+  if (mode == kLongLines2) {  // 2 rounds of whole 128-byte lines per lane in the LDS ring
+    const unsigned g = (unsigned)((n + 63) / 64);
+    if (bp) {
+      if (h2) fnv_fixed_lines_kernel<true, 2, 128, true><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, h2, *bp);
+      else fnv_fixed_lines_kernel<false, 2, 128, true><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr, *bp);
+    } else {
+      if (h2) fnv_fixed_lines_kernel<true, 2, 128><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, h2);
+      else fnv_fixed_lines_kernel<false, 2, 128><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+    }
+    return hipGetLastError();
+  }
+  const SpadTable t = make_spad(seed);
+  const unsigned g = (unsigned)((n + 255) / 256);
+  const BucketParams none{};
+  const BucketParams& p = bp ? *bp : none;
+  if (mode == kLongDirect) {  // per-lane direct loads (keys below 128 B)
+    if (bp) {
+      if (h2) fnv_fixed_long_kernel<true, true, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2, p);
+      else fnv_fixed_long_kernel<false, true, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr, p);
+    } else {
+      if (h2) fnv_fixed_long_kernel<true, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2);
+      else fnv_fixed_long_kernel<false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr);
+    }
+  } else {  // the cooperative line ring
+    if (bp) {
+      if (h2) fnv_fixed_long_kernel<true, false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2, p);
+      else fnv_fixed_long_kernel<false, false, true><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr, p);
+    } else {
+      if (h2) fnv_fixed_long_kernel<true, false><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, h2);
+      else fnv_fixed_long_kernel<false, false><<<g, 256, 0, stream>>>(k, key_len, n, t, h1, nullptr);
+    }
+  }
   return hipGetLastError();
 }
 

@@ -408,9 +408,13 @@ __global__ void scan_summary_kernel(const uint8_t* __restrict__ f, uint64_t size
 }
 
 // Scratch for the per-call temporaries: a library-private stream-ordered pool per device
-// whose release threshold keeps freed memory mapped (the default pool returns it at every
-// synchronisation, so each call would map its line / record arrays again).  The pool
-// holds at most the peak of one call's temporaries.
+// whose release threshold keeps up to kScratchKeep bytes of freed memory mapped (the
+// default pool returns everything at every synchronisation, so each call would map its
+// line / record arrays again).  Above the threshold, freed memory goes back to the device
+// at the next synchronisation, so a call over a huge file does not pin its peak for the
+// life of the process.
+constexpr uint64_t kScratchKeep = 256ull << 20;  // ~ the temporaries of a 1 GB file of 140-byte lines
+
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
   constexpr int kMaxDev = 64;
   static hipMemPool_t pools[kMaxDev] = {};
@@ -427,7 +431,7 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
     props.location.id = dev;
     hipMemPool_t pool = nullptr;
     if (hipMemPoolCreate(&pool, &props) != hipSuccess) return;
-    uint64_t keep = ~0ull;
+    uint64_t keep = kScratchKeep;
     (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     pools[dev] = pool;
   });

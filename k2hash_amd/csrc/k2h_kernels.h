@@ -11,9 +11,13 @@ namespace k2h {
 constexpr uint64_t kSeedBuiltinValue = 14695981039346656037ULL;  // lib/k2hashfunc.cc:51
 constexpr uint64_t kSeedStdValue = 2166136261ULL;                  // libstdc++ _Fnv_hash_impl seed
 
+// Kernel variant selector.  The product library (libk2hash_amd.so) always runs the
+// default kernel per shape (kVariantAuto); the measurement lab (K2H_AMD_LAB=1 build,
+// tools/lab/, k2h_amd_set_variant) compiles the round-1 A/B variants listed here.
+enum { kVariantAuto = 0 };
+#if K2H_AMD_LAB
 // Kernel variant selector (A/B measurement knob, K2H_AMD_VARIANT env / k2h_amd_set_variant).
 enum {
-  kVariantAuto = 0,      // best known kernel per shape
   kVariantCompiler = 1,  // fixed32: compiler-scheduled byte step instead of the hand-scheduled one
   kVariantGeneric = 2,   // fixed32: force the generic any-length kernel
   kVariantSimpleCsr = 3, // csr: one lane per key in input order (no length balancing)
@@ -79,6 +83,7 @@ enum {
   kVariantFixed32Pipe64 = 59,     // fixed32: persistent, next tile's loads issued before hashing the current
   kVariantFixed32Pipe256 = 60,    // (one-wave / 256-thread blocks, two keys per lane)
 };
+#endif
 
 // Bucket-index epilogue: where a hash lands in a k2hash table with
 // masks (cur_mask, collision_mask) -- the stateless part of K2HShm::GetKIndexPos
@@ -158,19 +163,25 @@ struct SpadTable {
 };
 SpadTable make_spad(uint64_t seed);
 
-// mode: 0 = tile staged in LDS by DMA (ring for oversize tiles), 1 = per-lane direct, 2 = ring only
+// CSR tile kernels (k2h_csr.hip).  The product mode: 512-key LDS-staged tiles hashed two keys
+// per lane, oversize tiles listed for a line-ring pass.  (Other modes: the lab build.)
+constexpr int kCsrDefaultMode = 11;
 hipError_t launch_csr_tile(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp = nullptr);
 // Long fixed-length keys: mode kLongAuto picks the line-DMA kernel (key_len % 128 == 0,
 // 128-aligned keys; 2 rounds of whole lines), else the cooperative line ring.
 // kLongHalfD: rounds of half lines (64 B per lane), D of them.
-enum { kLongAuto = 0, kLongDirect = 1, kLongRing = 2, kLongLines2 = 3, kLongLines3 = 4, kLongHalf3 = 5,
+enum { kLongAuto = 0, kLongDirect = 1, kLongRing = 2, kLongLines2 = 3,
+#if K2H_AMD_LAB
+       kLongLines3 = 4, kLongHalf3 = 5,
        kLongHalf4 = 6, kLongHalf6 = 7, kLongHalf5 = 8, kLongLines2Pad = 9, kLongLines2Pad2 = 10,
        kLongLines256 = 11,
        // timing probes (wrong hashes), keep last: no DMA / DMA only at (D, RB) =
        // (2,128) (2,128) (3,128) (4,128) (2,256) (4,64)
        kLongProbeCompute = 12, kLongProbeMemory = 13, kLongProbeMem3 = 14, kLongProbeMem4 = 15,
-       kLongProbeMem256 = 16, kLongProbeMemHalf4 = 17 };
+       kLongProbeMem256 = 16, kLongProbeMemHalf4 = 17
+#endif
+};
 bool fixed_lines_ok(const void* keys, uint64_t key_len);
 hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1,
                              uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp = nullptr);
@@ -179,8 +190,10 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
                         int variant, hipStream_t stream, const BucketParams* bp = nullptr);
 hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                       uint64_t* h2, int variant, hipStream_t stream, const BucketParams* bp = nullptr);
+#if K2H_AMD_LAB
 hipError_t launch_csr_simple(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                              uint64_t* h2, hipStream_t stream);
+#endif
 
 // Synthetic inputs (bench/test harness; same spec as oracle/fnv_oracle.c generators).
 hipError_t launch_synth_bytes(uint8_t* out, uint64_t nbytes, uint64_t seed, uint64_t byte_off, hipStream_t stream);

@@ -65,6 +65,7 @@ __device__ __forceinline__ uint4 ld_nt(const uint4* p) {
 }
 __device__ __forceinline__ void st_nt(uint64_t* p, uint64_t v) { __builtin_nontemporal_store(v, p); }
 
+#if K2H_AMD_LAB  // measurement-lab variants (tools/lab), not in libk2hash_amd.so
 // ---------------------------------------------------------------------------
 // fixed32: key i = keys[32*i .. 32*i+32), keys 16-byte aligned.
 // ---------------------------------------------------------------------------
@@ -123,6 +124,8 @@ __global__ __launch_bounds__(256) void fnv_fixed32_x_kernel(const uint4* __restr
   else fnv_key32_x(keys + 2 * i, h1 + i, seed);
 }
 
+#endif  // K2H_AMD_LAB
+
 // ---------------------------------------------------------------------------
 // fixed: key i = base[L*i .. L*i+L), any L >= 1, any alignment.  The loop trip
 // count is wave-uniform (L is a kernel argument), so no lane diverges.
@@ -166,11 +169,6 @@ __global__ __launch_bounds__(256) void fill_zero_kernel(uint64_t* __restrict__ p
 
 static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
-// ---------------------------------------------------------------------------
-// fixed32, persistent: 8 blocks of 256 threads per CU (8 waves/SIMD), each thread
-// strides over keys and loads its next key while hashing the current one, so a
-// wave's HBM latency hides under its own VALU work as well as other waves'.
-// ---------------------------------------------------------------------------
 __device__ __forceinline__ void fixed32_hash_store(uint4 a, uint4 b, uint64_t seed, uint64_t i, uint64_t* h1,
                                                    uint64_t* h2, bool want_h2) {
   uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2, hi2;
@@ -183,6 +181,7 @@ __device__ __forceinline__ void fixed32_hash_store(uint4 a, uint4 b, uint64_t se
   h1[i] = pack(lo, hi);
 }
 
+#if K2H_AMD_LAB  // measurement-lab variants (tools/lab), not in libk2hash_amd.so
 template <bool H2>
 __global__ __launch_bounds__(256) void fnv_fixed32_persist_kernel(const uint4* __restrict__ keys, uint64_t n,
                                                                   uint64_t seed, uint64_t* __restrict__ h1,
@@ -248,6 +247,10 @@ __global__ __launch_bounds__(256) void fnv_fixed32_lds_kernel(const uint4* __res
   }
 }
 
+
+
+#endif  // K2H_AMD_LAB
+
 // fixed32, flat grid, KPT keys per thread: block b owns keys [b*256*KPT, (b+1)*256*KPT);
 // thread t hashes keys b*256*KPT + j*256 + t.  All 2*KPT loads are issued before the
 // first hash, so each wave keeps KPT*2 KiB in flight while it computes.
@@ -291,6 +294,7 @@ __global__ __launch_bounds__(BS) void fnv_fixed32_kpt_kernel(const uint4* __rest
   }
 }
 
+#if K2H_AMD_LAB  // measurement-lab variants (tools/lab), not in libk2hash_amd.so
 // ---------------------------------------------------------------------------
 // fixed32, software-pipelined persistent blocks: each block walks tiles of 2*BS keys
 // (two keys per lane) with a grid stride, and the loads of its next tile are issued
@@ -489,13 +493,16 @@ static unsigned ring_grid(int variant, bool h2, uint64_t ntiles) {
   return (unsigned)(ntiles < g ? ntiles : g);
 }
 
+#endif  // K2H_AMD_LAB
+
 hipError_t launch_bucket_index(const uint64_t* h1, uint64_t n, const BucketParams& bp, hipStream_t stream) {
   if (n == 0 || !(bp.kindex || bp.ckindex)) return hipSuccess;
   bucket_index_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n, bp);
   return hipGetLastError();
 }
 
-hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
+#if K2H_AMD_LAB
+static hipError_t launch_fixed_lab(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
                         int variant, hipStream_t stream, const BucketParams* bp) {
   if (n == 0) return hipSuccess;
   const bool epi = bp && (bp->kindex || bp->ckindex);
@@ -663,7 +670,56 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
   }
   return hipGetLastError();
 }
+#endif  // K2H_AMD_LAB
 
+// Default kernel per shape (the product path).  32-byte keys at a 16-aligned base: one-wave
+// blocks, two keys per lane with all four loads issued before the first hash (a wave keeps
+// 4 KiB in flight and half as many waves need dispatching; round-1 A/B).
+// Other lengths (tools/fixed_sweep.py): up to 32 B the per-lane tail loop, below 128 B
+// per-lane direct 16-byte loads, from 128 B on the line-DMA kernel (multiples of 128 B at a
+// 128-aligned base) or the cooperative line ring.
+hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
+                        int variant, hipStream_t stream, const BucketParams* bp) {
+  if (n == 0) return hipSuccess;
+  const bool epi = bp && (bp->kindex || bp->ckindex);
+  if (!keys || key_len == 0) {
+    fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n);
+    if (h2) fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h2, n);
+    if (epi) return launch_bucket_index(h1, n, *bp, stream);
+    return hipGetLastError();
+  }
+#if K2H_AMD_LAB
+  if (variant != kVariantAuto) return launch_fixed_lab(keys, key_len, n, seed, h1, h2, variant, stream, bp);
+#else
+  (void)variant;
+#endif
+  if (key_len == 32 && ((uintptr_t)keys & 15u) == 0) {
+    const uint4* k = (const uint4*)keys;
+    const unsigned g = (unsigned)((n + 127) / 128);
+    if (epi) {
+      if (h2) fnv_fixed32_kpt_kernel<true, 2, 64, true, true><<<g, 64, 0, stream>>>(k, n, seed, h1, h2, *bp);
+      else fnv_fixed32_kpt_kernel<false, 2, 64, true, true><<<g, 64, 0, stream>>>(k, n, seed, h1, nullptr, *bp);
+    } else {
+      if (h2) fnv_fixed32_kpt_kernel<true, 2, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, h2);
+      else fnv_fixed32_kpt_kernel<false, 2, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, nullptr);
+    }
+    return hipGetLastError();
+  }
+  if (key_len > 32)
+    return launch_fixed_long(keys, key_len, n, seed, h1, h2, key_len < 128 ? kLongDirect : kLongAuto, stream,
+                             epi ? bp : nullptr);
+  const uint8_t* kb = (const uint8_t*)keys;
+  if (epi) {
+    if (h2) fnv_fixed_kernel<true, true><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, h2, *bp);
+    else fnv_fixed_kernel<false, true><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, nullptr, *bp);
+  } else {
+    if (h2) fnv_fixed_kernel<true><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, h2);
+    else fnv_fixed_kernel<false><<<grid_for(n), 256, 0, stream>>>(kb, key_len, n, seed, h1, nullptr);
+  }
+  return hipGetLastError();
+}
+
+#if K2H_AMD_LAB
 // ---------------------------------------------------------------------------
 // csr v0: one lane per key in input order (no length balancing).
 // ---------------------------------------------------------------------------
@@ -712,7 +768,7 @@ hipError_t launch_csr_simple(const void* bytes, const uint64_t* offsets, uint64_
   return hipGetLastError();
 }
 
-hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                       uint64_t* h2, int variant, hipStream_t stream, const BucketParams* bp) {
   if (n == 0) return hipSuccess;
   const bool epi = bp && (bp->kindex || bp->ckindex);
@@ -738,6 +794,27 @@ hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, ui
                          : variant == kVariantCsrLean2Group ? 14
                                                         : 11,
                          stream, epi ? bp : nullptr);
+}
+#endif  // K2H_AMD_LAB
+
+// CSR keys: 512-key tiles staged in LDS and hashed two keys per lane (k2h_csr.hip); a NULL
+// byte buffer hashes every key to 0 (lib/k2hashfunc.cc:66-68, 80-82).
+hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
+                      uint64_t* h2, int variant, hipStream_t stream, const BucketParams* bp) {
+  if (n == 0) return hipSuccess;
+  const bool epi = bp && (bp->kindex || bp->ckindex);
+#if K2H_AMD_LAB
+  if (variant != kVariantAuto) return launch_csr_lab(bytes, offsets, n, seed, h1, h2, variant, stream, bp);
+#else
+  (void)variant;
+#endif
+  if (!bytes) {
+    fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n);
+    if (h2) fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h2, n);
+    if (epi) return launch_bucket_index(h1, n, *bp, stream);
+    return hipGetLastError();
+  }
+  return launch_csr_tile(bytes, offsets, n, seed, h1, h2, kCsrDefaultMode, stream, epi ? bp : nullptr);
 }
 
 }  // namespace k2h

@@ -31,14 +31,16 @@ namespace {
 typedef uint64_t u64_ua __attribute__((aligned(1)));
 typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
 
+__device__ __forceinline__ uint64_t seg_len(const uint64_t* off, uint64_t i) { return off ? off[i + 1] - off[i] : 0; }
+__device__ __forceinline__ uint64_t seg_before(const uint64_t* off, uint64_t i) { return off ? off[i] - off[0] : 0; }
+
+#if K2H_AMD_LAB  // one thread per record (A/B variant)
 __device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len) {
   uint64_t j = 0;
   for (; j + 16 <= len; j += 16) *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
   for (; j < len; ++j) dst[j] = src[j];
 }
 
-__device__ __forceinline__ uint64_t seg_len(const uint64_t* off, uint64_t i) { return off ? off[i + 1] - off[i] : 0; }
-__device__ __forceinline__ uint64_t seg_before(const uint64_t* off, uint64_t i) { return off ? off[i] - off[0] : 0; }
 
 __global__ __launch_bounds__(256) void ralledata_assemble_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
                                                                  uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
@@ -68,6 +70,8 @@ __global__ __launch_bounds__(256) void ralledata_assemble_kernel(RalleInputs in,
     if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
   }
 }
+
+#endif
 
 // Group form (default): G lanes per record, 64/G records per wave.  Lane q of a group
 // writes header piece q (5 x 16 B) and copies bytes [16q + 16Gj, +16) of each segment,
@@ -129,6 +133,7 @@ __global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, ui
   }
 }
 
+#if K2H_AMD_LAB
 // Batched form (A/B variants 57-58, measured slower: 1.56 ms at 2 and 2.13 ms at 4 records
 // per group vs 1.50 for the group form -- the register cost (82 / 152 VGPRs) outweighs the
 // extra loads in flight).  Motivation: a header-only probe of the group form already
@@ -237,6 +242,8 @@ __global__ __launch_bounds__(256) void ralledata_batch_kernel(RalleInputs in, ui
   if (in.aoff) segment(3);
 }
 
+#endif  // K2H_AMD_LAB
+
 }  // namespace
 
 hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, uint8_t* out, uint64_t* blob_off,
@@ -250,6 +257,7 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
   if (e != hipSuccess) return e;
   e = launch_csr(in.keys, in.koff, n, seed, h, h + n, variant, stream);
   if (e == hipSuccess) {
+#if K2H_AMD_LAB
     if (variant == kVariantRalleThread)
       ralledata_assemble_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     else if (variant == kVariantRalleProbeAligned)
@@ -265,6 +273,7 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
     else if (variant == kVariantRalleBatch2)
       ralledata_batch_kernel<8, 2><<<(unsigned)(((n + 1) / 2 * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     else
+#endif
       ralledata_group_kernel<8><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     e = hipGetLastError();
   }

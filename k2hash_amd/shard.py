@@ -49,37 +49,59 @@ def rebase_offsets(offsets, first: int, last: int):
     return sub - sub[0]
 
 
-def gather_hashes(h, dst: int = 0, group=None, counts: Optional[list] = None):
-    """Gather every rank's hash vector to rank `dst` in rank (= key) order.
+def _global_rank(group, r: int) -> int:
+    """Global rank of group-local rank r (P2POp peers are global ranks)."""
+    import torch.distributed as dist
 
-    `h` is this rank's int64 tensor; `counts` (per-rank lengths) defaults to equal
-    lengths.  Returns the concatenated tensor on dst, None elsewhere.  Implemented as
-    point-to-point sends to the root (RCCL has no native gather; each peer uses its own
-    xGMI link to the root), posted together so they overlap.
+    return r if group is None else dist.get_global_rank(group, r)
+
+
+def shard_counts(n: int, world: int) -> list:
+    """Per-rank key counts of shard_range(n, r, world), r = 0..world-1."""
+    return [b - a for a, b in (shard_range(n, r, world) for r in range(world))]
+
+
+def gather_hashes(h, dst: int = 0, group=None, counts: Optional[list] = None):
+    """Gather every rank's hash vector to rank `dst` (group-local) in rank (= key) order.
+
+    `h` is this rank's int64 tensor.  `counts` (per-rank lengths, e.g. shard_counts) is
+    exchanged with one small all-gather when not given, so uneven shards work either way.
+    Returns the concatenated tensor on dst, None elsewhere.  Implemented as point-to-point
+    sends to the root (RCCL has no native gather; each peer uses its own xGMI link to the
+    root), posted together so they overlap.  Over gloo, device tensors are staged
+    through host memory (gloo's point-to-point ops take CPU tensors).
     """
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    staged = dist.get_backend(group) == "gloo" and h.is_cuda
+    hh = h.detach().cpu() if staged else h.contiguous()
     if counts is None:
-        counts = [h.numel()] * world
+        mine = torch.tensor([h.numel()], dtype=torch.int64, device="cpu" if (staged or not h.is_cuda) else h.device)
+        allc = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allc, mine, group=group)
+        counts = [int(c.item()) for c in allc]
+    if len(counts) != world or counts[rank] != h.numel():
+        raise ValueError("counts must list every rank's length")
     if rank == dst:
-        out = torch.empty(sum(counts), dtype=h.dtype, device=h.device)
+        out = torch.empty(sum(counts), dtype=h.dtype, device=hh.device)
         pieces = list(torch.split(out, counts))
         ops = []
         for r in range(world):
             if r == dst:
-                pieces[r].copy_(h)
-            else:
-                ops.append(dist.P2POp(dist.irecv, pieces[r], r, group))
+                pieces[r].copy_(hh)
+            elif counts[r]:
+                ops.append(dist.P2POp(dist.irecv, pieces[r], _global_rank(group, r), group))
         if ops:
             for req in dist.batch_isend_irecv(ops):
                 req.wait()
-        return out
-    reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, h.contiguous(), dst, group)])
-    for req in reqs:
-        req.wait()
+        return out.to(h.device) if staged else out
+    if h.numel():
+        reqs = dist.batch_isend_irecv([dist.P2POp(dist.isend, hh, _global_rank(group, dst), group)])
+        for req in reqs:
+            req.wait()
     return None
 
 
@@ -89,6 +111,8 @@ def all_gather_hashes(h, group=None):
     import torch.distributed as dist
 
     world = dist.get_world_size(group)
-    out = torch.empty(h.numel() * world, dtype=h.dtype, device=h.device)
-    dist.all_gather_into_tensor(out, h.contiguous(), group=group)
-    return out
+    staged = dist.get_backend(group) == "gloo" and h.is_cuda
+    hh = h.detach().cpu() if staged else h.contiguous()
+    out = torch.empty(h.numel() * world, dtype=h.dtype, device=hh.device)
+    dist.all_gather_into_tensor(out, hh, group=group)
+    return out.to(h.device) if staged else out

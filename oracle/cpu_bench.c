@@ -58,13 +58,14 @@ struct fixed_job {
   uint64_t key_len, first, count;
   int passes, want_h2;
   uint64_t digest;
-  pthread_barrier_t* bar;
+  pthread_barrier_t *ready, *go;
 };
 
 static void* fixed_worker(void* a) {
   struct fixed_job* j = (struct fixed_job*)a;
   uint64_t d = 0;
-  pthread_barrier_wait(j->bar);
+  pthread_barrier_wait(j->ready); /* started and parked: thread creation is outside the clock */
+  pthread_barrier_wait(j->go);
   for (int p = 0; p < j->passes; ++p) {
     const uint8_t* k = j->keys + j->first * j->key_len;
     for (uint64_t i = 0; i < j->count; ++i, k += j->key_len) {
@@ -76,7 +77,9 @@ static void* fixed_worker(void* a) {
   return NULL;
 }
 
-/* Returns wall seconds over all threads, or < 0 on error.  *digest = xor of per-thread digests. */
+/* Returns wall seconds over all threads from the release of the parked workers to the last
+ * join (`passes` passes over each thread's shard), or < 0 on error.  *digest = xor of
+ * per-thread digests. */
 double cpu_bench_fixed(const char* so, const uint8_t* keys, uint64_t key_len, uint64_t n, int threads, int passes,
                        int want_h2, uint64_t* digest) {
   hash_fn h1, h2;
@@ -84,22 +87,25 @@ double cpu_bench_fixed(const char* so, const uint8_t* keys, uint64_t key_len, ui
   if (threads < 1) threads = 1;
   struct fixed_job* jobs = (struct fixed_job*)calloc((size_t)threads, sizeof *jobs);
   pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof *th);
-  pthread_barrier_t bar;
-  pthread_barrier_init(&bar, NULL, (unsigned)threads + 1);
+  pthread_barrier_t ready, go;
+  pthread_barrier_init(&ready, NULL, (unsigned)threads + 1);
+  pthread_barrier_init(&go, NULL, (unsigned)threads + 1);
   for (int t = 0; t < threads; ++t) {
     uint64_t a = n * (uint64_t)t / (uint64_t)threads, b = n * (uint64_t)(t + 1) / (uint64_t)threads;
-    jobs[t] = (struct fixed_job){h1, h2, keys, key_len, a, b - a, passes, want_h2, 0, &bar};
+    jobs[t] = (struct fixed_job){h1, h2, keys, key_len, a, b - a, passes, want_h2, 0, &ready, &go};
     pthread_create(&th[t], NULL, fixed_worker, &jobs[t]);
   }
+  pthread_barrier_wait(&ready);
   double t0 = now();
-  pthread_barrier_wait(&bar);
+  pthread_barrier_wait(&go);
   uint64_t d = 0;
   for (int t = 0; t < threads; ++t) {
     pthread_join(th[t], NULL);
     d ^= jobs[t].digest;
   }
   double dt = now() - t0;
-  pthread_barrier_destroy(&bar);
+  pthread_barrier_destroy(&ready);
+  pthread_barrier_destroy(&go);
   free(jobs);
   free(th);
   if (digest) *digest = d;

@@ -1,0 +1,56 @@
+"""bench.py's launcher and multi-rank path.
+
+The driver runs `python bench.py --gpus N` (or the same under torch.distributed.run); with
+no RANK / WORLD_SIZE in the environment bench.py starts its own N ranks before touching a
+GPU.  On CPU the plumbing is rehearsed with the scalar plugin over gloo; on the GPU box two
+ranks share cuda:0 (gloo, device tensors staged through host memory) and run the real
+kernels, the digest checks and the gather."""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+
+
+def _run(args, timeout):
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py")] + args, capture_output=True, text=True,
+                       timeout=timeout, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+def test_launcher_rehearsal_cpu():
+    line = _run(["--gpus", "2", "--rehearse-cpu", "--backend", "gloo", "--steps", "2", "--warmup", "1",
+                 "--keys", "777"], 240)
+    assert line["n_gpus"] == 2 and line["gather"]["ok"] is True
+    assert "NOT a measurement" in line["device"]
+
+
+def test_launcher_rehearsal_cpu_three_ranks():
+    line = _run(["--gpus", "3", "--rehearse-cpu", "--backend", "gloo", "--steps", "1", "--warmup", "0",
+                 "--keys", "1001"], 240)
+    assert line["n_gpus"] == 3 and line["gather"]["ok"] is True
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_gpu():
+    """Config 4's path at N=2 on one card: strong-scaled shards of a small key count, the
+    gather of both shards' hashes and the hash+gather step."""
+    line = _run(["--gpus", "2", "--backend", "gloo", "--keys", "262144", "--steps", "5", "--warmup", "1",
+                 "--warm-ms", "5"], 600)
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["gather"]["with_gather"]["value"] > 0 and line["gather"]["backend"] == "gloo"
+
+
+@pytest.mark.gpu
+def test_bench_n1_headline_verified():
+    line = _run(["--steps", "5", "--warmup", "2", "--warm-ms", "10", "--no-secondary", "--no-cpu-baseline"], 600)
+    assert line["n_gpus"] == 1 and line["verify"]["ok"] is True
+    assert 0 < line["roofline"]["frac"] < 1 and 0 < line["roofline"]["valu_frac"] < 1.2

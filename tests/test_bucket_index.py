@@ -90,52 +90,40 @@ def test_standalone_optional_outputs_and_errors(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 4, 12, 16])
-@pytest.mark.parametrize("key_len", [32, 21, 4096, 100])
-def test_fused_fixed_vs_oracle(cuda, oracle, key_len, variant):
+@pytest.mark.parametrize("key_len", [32, 21, 4096, 100, 256])
+def test_fused_fixed_vs_oracle(cuda, oracle, key_len):
     import torch
-    if key_len != 32 and variant != 0:
-        pytest.skip("A/B variants only differ for 32-byte keys")
-    batch.set_variant(variant)
-    try:
-        n = 70001 if key_len < 1000 else 3001
-        data = oracle.gen_bytes(key_len * n, byte_off=99)
-        r1, r2 = oracle.hash_fixed(data, key_len)
-        keys = torch.from_numpy(data).to(cuda)
-        for cur, cm in [(0xFF, 0xF), ((1 << 28) - 1, 0xF), (0x3, 0x3)]:
-            h1, h2, k, c = k2hash_amd.hash_fixed_index(keys, key_len, cur, cm, second=True)
-            torch.cuda.synchronize()
-            rk, rc = oracle.bucket_index(r1, cur, cm)
-            assert np.array_equal(h1.cpu().numpy().view(np.uint64), r1)
-            assert np.array_equal(h2.cpu().numpy().view(np.uint64), r2)
-            assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
-            assert np.array_equal(c.cpu().numpy().view(np.uint64), rc)
-    finally:
-        batch.set_variant(0)
+    n = 70001 if key_len < 1000 else 3001
+    data = oracle.gen_bytes(key_len * n, byte_off=99)
+    r1, r2 = oracle.hash_fixed(data, key_len)
+    keys = torch.from_numpy(data).to(cuda)
+    for cur, cm in [(0xFF, 0xF), ((1 << 28) - 1, 0xF), (0x3, 0x3)]:
+        h1, h2, k, c = k2hash_amd.hash_fixed_index(keys, key_len, cur, cm, second=True)
+        torch.cuda.synchronize()
+        rk, rc = oracle.bucket_index(r1, cur, cm)
+        assert np.array_equal(h1.cpu().numpy().view(np.uint64), r1)
+        assert np.array_equal(h2.cpu().numpy().view(np.uint64), r2)
+        assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
+        assert np.array_equal(c.cpu().numpy().view(np.uint64), rc)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("variant", [0, 3, 11, 19, 54])
-def test_fused_csr_vs_oracle(cuda, oracle, variant):
+def test_fused_csr_vs_oracle(cuda, oracle):
     import torch
-    batch.set_variant(variant)
-    try:
-        rng = np.random.default_rng(11)
-        L = rng.integers(0, 300, 20000)
-        L[::17] = 0
-        off = np.zeros(L.size + 1, np.int64)
-        off[1:] = np.cumsum(L)
-        data = oracle.gen_bytes(int(off[-1]) + 3)
-        r1, _ = oracle.hash_csr(data, off.astype(np.uint64))
-        h1, h2, k, c = k2hash_amd.hash_csr_index(torch.from_numpy(data).to(cuda), torch.from_numpy(off).to(cuda),
-                                                 0xFFFF, 0xF, ckindex=False)
-        torch.cuda.synchronize()
-        rk, _ = oracle.bucket_index(r1, 0xFFFF, 0xF)
-        assert h2 is None and c is None
-        assert np.array_equal(h1.cpu().numpy().view(np.uint64), r1)
-        assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
-    finally:
-        batch.set_variant(0)
+    rng = np.random.default_rng(11)
+    L = rng.integers(0, 300, 20000)
+    L[::17] = 0
+    off = np.zeros(L.size + 1, np.int64)
+    off[1:] = np.cumsum(L)
+    data = oracle.gen_bytes(int(off[-1]) + 3)
+    r1, _ = oracle.hash_csr(data, off.astype(np.uint64))
+    h1, h2, k, c = k2hash_amd.hash_csr_index(torch.from_numpy(data).to(cuda), torch.from_numpy(off).to(cuda),
+                                             0xFFFF, 0xF, ckindex=False)
+    torch.cuda.synchronize()
+    rk, _ = oracle.bucket_index(r1, 0xFFFF, 0xF)
+    assert h2 is None and c is None
+    assert np.array_equal(h1.cpu().numpy().view(np.uint64), r1)
+    assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
 
 
 @pytest.mark.gpu

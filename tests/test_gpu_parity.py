@@ -16,9 +16,6 @@ from k2hash_amd import batch
 
 pytestmark = pytest.mark.gpu
 
-VARIANTS = [0, 1, 2, 4, 5, 6, 7, 8, 12, 16, 17, 18, 23, 24, 25, 26, 27, 29, 30, 31, 59, 60]
-CSR_VARIANTS = [0, 3, 10, 11, 13, 14, 19, 20, 21, 48, 51, 52, 53, 54]
-
 
 def dev_u8(torch, arr, device, pad_front=0):
     """Device copy of a host byte array, optionally starting `pad_front` bytes into
@@ -32,17 +29,9 @@ def host_u64(t):
     return t.cpu().numpy().view(np.uint64)
 
 
-@pytest.fixture(autouse=True)
-def _reset_variant():
-    yield
-    batch.set_variant(0)
-
-
-@pytest.mark.parametrize("variant", VARIANTS)
-@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 255, 257, 4099, 100003])
-def test_fixed32_vs_oracle(cuda, oracle, n, variant):
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 128, 129, 255, 257, 4099, 100003])
+def test_fixed32_vs_oracle(cuda, oracle, n):
     import torch
-    batch.set_variant(variant)
     data = oracle.gen_bytes(32 * n, byte_off=32 * 12345)
     r1, r2 = oracle.hash_fixed(data, 32)
     keys = dev_u8(torch, data, cuda)
@@ -54,13 +43,10 @@ def test_fixed32_vs_oracle(cuda, oracle, n, variant):
     assert np.array_equal(host_u64(g1), r1)
 
 
-@pytest.mark.parametrize("variant", [0, 5, 6, 16, 17, 18, 59, 60])
 @pytest.mark.parametrize("n", [(1 << 21) + 17, 3 << 20])
-def test_fixed32_persistent_many_tiles(cuda, oracle, n, variant):
-    """Persistent / ring kernels at sizes where every wave walks many tiles (the
-    small cases above give most waves a single tile)."""
+def test_fixed32_many_blocks(cuda, oracle, n):
+    """Millions of keys hash for hash (the digests below cover the full sizes)."""
     import torch
-    batch.set_variant(variant)
     data = oracle.gen_bytes(32 * n, byte_off=32 * 777)
     r1, r2 = oracle.hash_fixed(data, 32)
     keys = dev_u8(torch, data, cuda)
@@ -93,10 +79,8 @@ def _csr(keys):
     return data, off
 
 
-@pytest.mark.parametrize("variant", CSR_VARIANTS)
-def test_golden_vectors_csr(cuda, vectors, variant):
+def test_golden_vectors_csr(cuda, vectors):
     import torch
-    batch.set_variant(variant)
     for field, std in (("vectors", False), ("std_fnv_vectors", True)):
         vs = vectors[field]
         data, off = _csr([hexkey(v) for v in vs])
@@ -108,11 +92,9 @@ def test_golden_vectors_csr(cuda, vectors, variant):
             assert (int(a[i]), int(b[i])) == (u64(v["h1"]), u64(v["h2"])), (field, v["tag"], v["len"])
 
 
-@pytest.mark.parametrize("variant", CSR_VARIANTS)
 @pytest.mark.parametrize("lens", ["mixed", "zeros", "long", "uniform"])
-def test_csr_vs_oracle(cuda, oracle, lens, variant):
+def test_csr_vs_oracle(cuda, oracle, lens):
     import torch
-    batch.set_variant(variant)
     rng = np.random.default_rng(5)
     if lens == "mixed":
         L = rng.integers(0, 300, 6000)
@@ -218,11 +200,9 @@ def test_full_size_fixed_digest(cuda, oracle, digests, name):
     assert torch.equal(g1, h1)
 
 
-@pytest.mark.parametrize("variant", [0, 19, 20, 21, 48, 54])
 @pytest.mark.parametrize("name", ["csr_8_256_64M", "csr_8_256_64K"])
-def test_full_size_csr_digest(cuda, oracle, digests, name, variant):
+def test_full_size_csr_digest(cuda, oracle, digests, name):
     import torch
-    batch.set_variant(variant)
     cfg = digests[name]
     off = batch.synth_offsets(cfg["n"], cuda, cfg["min_len"], cfg["max_len"])
     data = batch.synth_bytes(int(off[-1].item()), cuda)
@@ -244,17 +224,18 @@ def test_config4_shard_digests(cuda, oracle, digests):
         del keys, h1, h2
 
 
-@pytest.mark.parametrize("variant", [32, 33, 34, 35, 36, 37, 38, 39, 40, 47])
-@pytest.mark.parametrize("key_len,n", [(128, 1), (128, 64), (256, 517), (384, 130), (1024, 200), (4096, 67)])
-def test_fixed_long_kernels_vs_oracle(cuda, oracle, variant, key_len, n):
-    """Long fixed-length keys: the line ring (32) and the line-DMA ring kernels (33-35,
-    2/3/4 rounds), partial last waves included; h1 and h2."""
+@pytest.mark.parametrize("pad", [0, 16])
+@pytest.mark.parametrize("key_len,n", [(128, 1), (128, 64), (256, 517), (384, 130), (1024, 200), (4096, 67),
+                                       (4096, 1000), (200, 300)])
+def test_fixed_long_kernels_vs_oracle(cuda, oracle, key_len, n, pad):
+    """Long fixed-length keys: the line-DMA ring kernel (multiples of 128 B at a 128-aligned
+    base) and the cooperative line ring (any other base or length), partial last waves
+    included; h1 and h2."""
     import torch
     data = oracle.gen_bytes(key_len * n, byte_off=3 * key_len + 1)
     r1, r2 = oracle.hash_fixed(data, key_len)
-    batch.set_variant(variant)
-    keys = dev_u8(torch, data, cuda)
-    assert keys.data_ptr() % 128 == 0
+    keys = dev_u8(torch, data, cuda, pad_front=pad)
+    assert (keys.data_ptr() % 128 == 0) == (pad == 0)
     h1, h2 = k2hash_amd.hash_fixed(keys, key_len, second=True)
     g1, _ = k2hash_amd.hash_fixed(keys, key_len)
     torch.cuda.synchronize()

@@ -2,8 +2,9 @@
 with the gloo backend at world_size 2 (and 3 for uneven splits).  The same code runs
 over RCCL ("nccl") with device tensors in bench.py --gpus N.
 
-Per-rank hashes here come from the product's scalar path (k2hash_amd.k2h_hash, the
-plugin body) since there is no GPU; the gathered vector is checked against the oracle."""
+Per-rank hashes come from the product's scalar path (k2hash_amd.k2h_hash, the plugin
+body) on CPU, and from the HIP kernel in the gpu-marked test; the gathered vector is
+checked against the oracle."""
 import os
 import socket
 
@@ -50,7 +51,11 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n, key_len, q):
+def _worker(rank, world, port, n, key_len, q, mode="cpu"):
+    """mode: "cpu" (scalar plugin hashes, counts given), "auto" (counts exchanged by
+    gather_hashes itself), "subgroup" (gather inside the group of global ranks 1..world-1
+    to its local rank 0), "gpu" (hashes computed by the HIP kernel on cuda:0, device
+    tensors gathered over gloo)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -62,35 +67,75 @@ def _worker(rank, world, port, n, key_len, q):
         import oracle
         first, last = shard.shard_range(n, rank, world)
         data = oracle.gen_bytes((last - first) * key_len, byte_off=first * key_len)
-        h = torch.tensor([k2hash_amd.k2h_hash(data[i * key_len:(i + 1) * key_len].tobytes())
-                          for i in range(last - first)], dtype=torch.uint64).view(torch.int64)
-        counts = [shard.shard_range(n, r, world)[1] - shard.shard_range(n, r, world)[0] for r in range(world)]
-        out = shard.gather_hashes(h, dst=0, counts=counts)
+        if mode == "gpu":
+            keys = torch.from_numpy(data).to("cuda:0")
+            h, _ = k2hash_amd.hash_fixed(keys, key_len)
+            torch.cuda.synchronize()
+        else:
+            h = torch.tensor([k2hash_amd.k2h_hash(data[i * key_len:(i + 1) * key_len].tobytes())
+                              for i in range(last - first)], dtype=torch.uint64).view(torch.int64)
+        counts = shard.shard_counts(n, world)
+        if mode == "subgroup":
+            members = list(range(1, world))
+            grp = dist.new_group(members)
+            if rank in members:
+                out = shard.gather_hashes(h, dst=0, group=grp)
+                if rank == 1:
+                    q.put(("sub", out.numpy().copy()))
+            dist.barrier()
+            return
+        out = shard.gather_hashes(h, dst=0, counts=None if mode == "auto" else counts)
         if rank == 0:
-            q.put(out.view(torch.uint64).numpy().copy() if hasattr(torch, "uint64") else out.numpy().copy())
+            q.put(out.cpu().numpy().copy())
         if len(set(counts)) == 1:
             allh = shard.all_gather_hashes(h)
-            q.put((rank, allh.numpy().copy()))
+            q.put((rank, allh.cpu().numpy().copy()))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,n", [(2, 1000), (3, 1001)])
-def test_gather_hashes_gloo(oracle, world, n):
-    key_len = 32
+def _run(world, n, key_len, mode, expect):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, key_len, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, key_len, q, mode)) for r in range(world)]
     for p in procs:
         p.start()
-    results = [q.get(timeout=120) for _ in range(1 + (world if n % world == 0 else 0))]
+    results = [q.get(timeout=180) for _ in range(expect)]
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return results
+
+
+@pytest.mark.parametrize("world,n,mode", [(2, 1000, "cpu"), (3, 1001, "cpu"), (3, 1001, "auto")])
+def test_gather_hashes_gloo(oracle, world, n, mode):
+    key_len = 32
+    results = _run(world, n, key_len, mode, 1 + (world if n % world == 0 else 0))
     ref, _ = oracle.hash_fixed(oracle.gen_bytes(n * key_len), key_len)
     gathered = [r for r in results if not isinstance(r, tuple)][0]
     assert np.array_equal(np.asarray(gathered).view(np.uint64), ref)
     for r in results:
         if isinstance(r, tuple):
             assert np.array_equal(r[1].view(np.uint64), ref)
+
+
+def test_gather_hashes_subgroup(oracle):
+    """A non-default group: peers are translated to global ranks."""
+    world, n, key_len = 3, 999, 32
+    (tag, got), = _run(world, n, key_len, "subgroup", 1)
+    ref, _ = oracle.hash_fixed(oracle.gen_bytes(n * key_len), key_len)
+    lo = shard.shard_range(n, 1, world)[0]
+    assert tag == "sub" and np.array_equal(got.view(np.uint64), ref[lo:])
+
+
+@pytest.mark.gpu
+def test_gather_hip_hashes(oracle):
+    """HIP-computed hashes (two ranks sharing cuda:0) through gather_hashes and
+    all_gather_hashes, staged over gloo; the gathered vector is the oracle's."""
+    world, n, key_len = 2, 200000, 32
+    results = _run(world, n, key_len, "gpu", 1 + world)
+    ref, _ = oracle.hash_fixed(oracle.gen_bytes(n * key_len), key_len)
+    gathered = [r for r in results if not isinstance(r, tuple)][0]
+    assert np.array_equal(np.asarray(gathered).view(np.uint64), ref)
+    assert all(np.array_equal(r[1].view(np.uint64), ref) for r in results if isinstance(r, tuple))

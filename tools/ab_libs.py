@@ -53,7 +53,8 @@ paths = [str(_native.BATCH_LIB)] + [x for x in a.libs.split(",") if x]
 libs = []
 for path in paths:
     lib = _native._bind(ctypes.CDLL(str(Path(path).resolve())), _native.SIGNATURES.keys())
-    lib.k2h_amd_set_variant(a.variant)
+    if a.variant:
+        lib.k2h_amd_set_variant(a.variant)
     libs.append(lib)
 
 

@@ -9,14 +9,17 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import torch  # noqa: E402
 
+import os  # noqa: E402
+os.environ.setdefault("K2H_AMD_BATCH_LIB", str(Path(__file__).resolve().parents[1] / "tools" / "lab" / "libk2hash_amd_lab.so"))
 import k2hash_amd  # noqa: E402
+from k2hash_amd import _native  # noqa: E402
 from k2hash_amd import batch  # noqa: E402
 
 dev = torch.device("cuda:0")
 n = 1 << 24
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 1000
 variant = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-batch.set_variant(variant)
+_native.lab_set_variant(variant)
 sets = [batch.synth_bytes(32 * n, dev, byte_off=s * 32 * n) for s in range(2)]
 outs = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(2)]
 

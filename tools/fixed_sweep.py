@@ -19,7 +19,10 @@ sys.path.insert(0, str(ROOT / "oracle"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+import os  # noqa: E402
+os.environ.setdefault("K2H_AMD_BATCH_LIB", str(Path(__file__).resolve().parents[1] / "tools" / "lab" / "libk2hash_amd_lab.so"))
 import k2hash_amd  # noqa: E402
+from k2hash_amd import _native  # noqa: E402
 from k2hash_amd import batch  # noqa: E402
 import oracle  # noqa: E402  (checker only)
 
@@ -38,7 +41,7 @@ for L in [int(x) for x in a.lens.split(",")]:
     out = torch.empty(n, dtype=torch.int64, device=dev)
     ref = oracle.hash_fixed(keys[: 4096 * L].cpu().numpy(), L)[0]
     for v in variants:
-        batch.set_variant(v)
+        _native.lab_set_variant(v)
         k2hash_amd.hash_fixed(keys, L, out=(out, None))
         torch.cuda.synchronize()
         if not np.array_equal(out[:4096].cpu().numpy().view(np.uint64), ref):
@@ -47,7 +50,7 @@ for L in [int(x) for x in a.lens.split(",")]:
     times = {v: [] for v in variants}
     for r in range(a.rounds):
         for v in variants:
-            batch.set_variant(v)
+            _native.lab_set_variant(v)
             for i in range(2):
                 k2hash_amd.hash_fixed(keys, L, out=(out, None))
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -64,4 +67,4 @@ for L in [int(x) for x in a.lens.split(",")]:
         row[f"v{v}_frac"] = round((n * L + 8 * n) / med / 1e6 / 8000, 3)
     print(json.dumps(row), flush=True)
     del keys, out
-    batch.set_variant(0)
+    _native.lab_set_variant(0)

@@ -18,7 +18,10 @@ sys.path.insert(0, str(ROOT / "oracle"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
+import os  # noqa: E402
+os.environ.setdefault("K2H_AMD_BATCH_LIB", str(Path(__file__).resolve().parents[1] / "tools" / "lab" / "libk2hash_amd_lab.so"))
 import k2hash_amd  # noqa: E402
+from k2hash_amd import _native  # noqa: E402
 from k2hash_amd import batch  # noqa: E402
 import oracle  # noqa: E402  (checker only)
 
@@ -61,7 +64,7 @@ def run(i):
 
 variants = [int(v) for v in a.variants.split(",")]
 for v in variants:
-    batch.set_variant(v)
+    _native.lab_set_variant(v)
     run(0)
     torch.cuda.synchronize()
     d1 = oracle.digest(out[0].cpu().numpy().view(np.uint64))
@@ -73,7 +76,7 @@ for v in variants:
         sys.exit(1)
 
 import time  # noqa: E402
-batch.set_variant(variants[0])
+_native.lab_set_variant(variants[0])
 w0 = time.perf_counter()
 while time.perf_counter() - w0 < 0.3:  # past the clock ramp (profiles/r01_clock_ramp.txt)
     for i in range(10):
@@ -82,7 +85,7 @@ while time.perf_counter() - w0 < 0.3:  # past the clock ramp (profiles/r01_clock
 times = {v: [] for v in variants}
 for r in range(a.rounds):
     for v in variants:
-        batch.set_variant(v)
+        _native.lab_set_variant(v)
         for i in range(3):
             run(i)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
