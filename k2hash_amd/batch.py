@@ -179,13 +179,23 @@ def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 
 
+def _host_outs(n, second, out):
+    if out is not None:
+        h1, h2 = out
+        if h1.dtype != np.uint64 or h1.size != n or not h1.flags.c_contiguous or \
+                (second and (h2 is None or h2.dtype != np.uint64 or h2.size != n or not h2.flags.c_contiguous)):
+            raise ValueError("out must be contiguous uint64 arrays of n entries")
+        return h1, (h2 if second else None)
+    return np.empty(n, dtype=np.uint64), (np.empty(n, dtype=np.uint64) if second else None)
+
+
 def hash_fixed_host(keys: np.ndarray, key_len: int, second: bool = False, std_fnv: bool = False,
-                    device: int = 0):
-    """Host-memory form of hash_fixed (numpy uint8 in, numpy uint64 out)."""
+                    device: int = 0, out=None):
+    """Host-memory form of hash_fixed (numpy uint8 in, numpy uint64 out; `out`: reuse
+    (h1, h2) arrays)."""
     keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
     n = keys.size // key_len
-    h1 = np.empty(n, dtype=np.uint64)
-    h2 = np.empty(n, dtype=np.uint64) if second else None
+    h1, h2 = _host_outs(n, second, out)
     rc = _native.batch_lib().k2h_amd_hash_fixed_host(
         _np_ptr(keys), key_len, n, _np_ptr(h1), _np_ptr(h2) if h2 is not None else None,
         FLAG_STD_FNV if std_fnv else 0, device)
@@ -194,13 +204,12 @@ def hash_fixed_host(keys: np.ndarray, key_len: int, second: bool = False, std_fn
 
 
 def hash_csr_host(data: np.ndarray, offsets: np.ndarray, second: bool = False, std_fnv: bool = False,
-                  device: int = 0):
+                  device: int = 0, out=None):
     """Host-memory form of hash_csr."""
     data = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64).reshape(-1)
     n = offsets.size - 1
-    h1 = np.empty(n, dtype=np.uint64)
-    h2 = np.empty(n, dtype=np.uint64) if second else None
+    h1, h2 = _host_outs(n, second, out)
     dptr = _np_ptr(data) if data.size else ctypes.c_void_p(1)
     rc = _native.batch_lib().k2h_amd_hash_csr_host(
         dptr, _np_ptr(offsets), n, _np_ptr(h1), _np_ptr(h2) if h2 is not None else None,

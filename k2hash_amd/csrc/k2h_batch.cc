@@ -144,14 +144,25 @@ CopyPool& pool() {
 }
 
 // ---------------------------------------------------------------------------
-// Host-path staging context: per device, two pipeline slots.
+// Host-path pipeline: per device, two slots used alternately, one stream each.
+//  - in:  the caller's keys are copied into the slot's pinned staging buffer by the copy
+//         pool (8+ threads: ~119 GB/s, tools/host_probe.hip) while the previous chunk's
+//         H2D DMA runs, then DMA'd at the PCIe rate (57.5 GB/s).  Handing the runtime the
+//         caller's pageable buffer instead makes it pin the whole allocation on every call
+//         (~40 ms per 512 MiB, rocprofv3 --sys-trace of tools/host_trace.py).
+//  - out: fixed-length keys: the kernel stores the hashes straight into the slot's pinned
+//         output buffer over PCIe (a wave writes whole lines), so no D2H copy queues behind
+//         the next chunk's H2D on the DMA engine; CSR keys (hashes stored in length-sorted
+//         order, partial lines) come back with a D2H copy.  The pool then copies them to
+//         the caller when the slot is reused or the call ends.
 // ---------------------------------------------------------------------------
 struct Slot {
   hipStream_t stream = nullptr;
   hipEvent_t done = nullptr;
   uint8_t* h_in = nullptr;   // pinned input bytes
-  uint64_t* h_off = nullptr; // pinned rebased offsets (CSR)
+  uint64_t* h_off = nullptr; // pinned offsets (CSR)
   uint64_t* h_out = nullptr; // pinned h1 (+h2) results
+  uint64_t* h_out_dev = nullptr; // the same buffer as a device pointer (kernel stores)
   uint8_t* d_in = nullptr;
   uint64_t* d_off = nullptr;
   uint64_t* d_out = nullptr;
@@ -164,7 +175,6 @@ struct Slot {
 
 struct HostCtx {
   std::mutex mu;
-  int device = -1;
   Slot slot[2];
 };
 
@@ -196,6 +206,7 @@ int slot_reserve(Slot& s, uint64_t bytes, uint64_t keys) {
     if (s.d_out) (void)hipFree(s.d_out);
     s.h_off = nullptr;
     s.h_out = nullptr;
+    s.h_out_dev = nullptr;
     s.d_off = nullptr;
     s.d_out = nullptr;
     s.cap_keys = 0;
@@ -203,6 +214,7 @@ int slot_reserve(Slot& s, uint64_t bytes, uint64_t keys) {
         hipHostMalloc((void**)&s.h_out, keys * 16, hipHostMallocDefault) != hipSuccess ||
         hipMalloc((void**)&s.d_off, (keys + 1) * 8) != hipSuccess || hipMalloc((void**)&s.d_out, keys * 16) != hipSuccess)
       return fail(K2H_AMD_ENOMEM, "staging allocation (keys)");
+    if (hipHostGetDevicePointer((void**)&s.h_out_dev, s.h_out, 0) != hipSuccess) s.h_out_dev = nullptr;
     s.cap_keys = keys;
   }
   return K2H_AMD_OK;
@@ -385,10 +397,11 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed_host(const void* k
     if ((rc = slot_reserve(s, per * key_len, per))) return rc;
     pool().copy(s.h_in, src + first * key_len, cnt * key_len);
     hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, cnt * key_len, hipMemcpyHostToDevice, s.stream);
+    uint64_t* out = s.h_out_dev ? s.h_out_dev : s.d_out;  // kernel stores over PCIe when mapped
     if (e == hipSuccess)
-      e = k2h::launch_fixed(s.d_in, key_len, cnt, seed_for(flags), s.d_out, h2 ? s.d_out + cnt : nullptr, variant(),
-                            s.stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, cnt * (h2 ? 16 : 8), hipMemcpyDeviceToHost, s.stream);
+      e = k2h::launch_fixed(s.d_in, key_len, cnt, seed_for(flags), out, h2 ? out + cnt : nullptr, variant(), s.stream);
+    if (e == hipSuccess && !s.h_out_dev)
+      e = hipMemcpyAsync(s.h_out, s.d_out, cnt * (h2 ? 16 : 8), hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
     if (e != hipSuccess) return fail(K2H_AMD_EHIP, "fixed host chunk", e);
     s.busy = true;
@@ -411,8 +424,6 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* byt
     if (h2) memset(h2, 0, n * 8);
     return K2H_AMD_OK;
   }
-  for (uint64_t i = 0; i < n; ++i)
-    if (offsets[i + 1] < offsets[i]) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
   DeviceGuard dg;
   int rc = dg.enter(device);
   if (rc) return rc;
@@ -423,22 +434,29 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* byt
   int k = 0;
   uint64_t first = 0;
   while (first < n) {
-    // grow the chunk by keys until the byte budget or the key cap is reached (always >= 1 key)
-    uint64_t last = first + 1;
-    uint64_t cap_keys = first + kChunkKeysMax < n ? first + kChunkKeysMax : n;
-    while (last < cap_keys && offsets[last + 1] - offsets[first] <= kChunkBytes) ++last;
+    // the longest run of keys from `first` within the byte budget and the key cap (>= 1 key),
+    // by binary search; the run's offsets are then checked to be non-decreasing (the GPU
+    // still works on the previous chunk meanwhile)
+    const uint64_t cap = first + kChunkKeysMax < n ? first + kChunkKeysMax : n;
+    const uint64_t limit = offsets[first] + kChunkBytes;
+    uint64_t last = (uint64_t)(std::upper_bound(offsets + first + 1, offsets + cap + 1, limit) - offsets) - 1;
+    if (last <= first) last = first + 1;
+    for (uint64_t i = first; i < last; ++i)
+      if (offsets[i + 1] < offsets[i]) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
     uint64_t cnt = last - first;
     uint64_t nb = offsets[last] - offsets[first];
     Slot& s = c.slot[k];
     if ((rc = slot_drain(s, h1, h2))) return rc;
     if ((rc = slot_reserve(s, nb > kChunkBytes ? nb : kChunkBytes, kChunkKeysMax))) return rc;
+    // the kernel takes the caller's offsets as they are, relative to a byte base placed
+    // offsets[first] bytes before the chunk (no rebasing pass on the CPU)
     pool().copy(s.h_in, src + offsets[first], nb);
-    for (uint64_t i = 0; i <= cnt; ++i) s.h_off[i] = offsets[first + i] - offsets[first];
-    hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, nb, hipMemcpyHostToDevice, s.stream);
+    pool().copy(s.h_off, offsets + first, (cnt + 1) * 8);
+    hipError_t e = nb ? hipMemcpyAsync(s.d_in, s.h_in, nb, hipMemcpyHostToDevice, s.stream) : hipSuccess;
     if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess)
-      e = k2h::launch_csr(s.d_in, s.d_off, cnt, seed_for(flags), s.d_out, h2 ? s.d_out + cnt : nullptr, variant(),
-                          s.stream);
+      e = k2h::launch_csr((const uint8_t*)s.d_in - offsets[first], s.d_off, cnt, seed_for(flags), s.d_out,
+                          h2 ? s.d_out + cnt : nullptr, variant(), s.stream);
     if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, cnt * (h2 ? 16 : 8), hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
     if (e != hipSuccess) return fail(K2H_AMD_EHIP, "csr host chunk", e);

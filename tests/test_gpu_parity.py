@@ -242,3 +242,25 @@ def test_fixed_long_kernels_vs_oracle(cuda, oracle, key_len, n, pad):
     assert np.array_equal(host_u64(h1), r1)
     assert np.array_equal(host_u64(h2), r2)
     assert np.array_equal(host_u64(g1), r1)
+
+
+def test_host_api_error_mid_call_leaves_no_stale_chunk(cuda, oracle):
+    """a host call that fails after launching chunks (here: offsets that stop
+    being non-decreasing inside the second 4M-key chunk) must not leave a pending chunk
+    that a later call drains into its own output."""
+    from k2hash_amd import _native
+    n = (4 << 20) + 64
+    off = np.arange(n + 1, dtype=np.uint64)  # one-byte keys
+    data = oracle.gen_bytes(n)
+    bad = off.copy()
+    bad[(4 << 20) + 10] = 0
+    with pytest.raises(_native.NativeError):
+        k2hash_amd.hash_csr_host(data, bad)
+    m = 1000
+    small = oracle.gen_offsets(m, 1, 40)
+    sdata = oracle.gen_bytes(int(small[-1]), byte_off=77)
+    h1, h2 = k2hash_amd.hash_csr_host(sdata, small, second=True)
+    r1, r2 = oracle.hash_csr(sdata, small)
+    assert np.array_equal(h1, r1) and np.array_equal(h2, r2)
+    g1, _ = k2hash_amd.hash_csr_host(data, off)  # and the full call still works
+    assert np.array_equal(g1, oracle.hash_csr(data, off)[0])

@@ -1,32 +1,33 @@
 #!/bin/bash
-# Round profile: bench lines for configs 2/3/5, rocprofv3 kernel stats of the same
-# commands, and FETCH_SIZE / WRITE_SIZE PMC passes (separate runs, kernel-trace only).
-# Usage: OUT=gpurun_out/prof_rNN TAG=rNN bash tools/profile_round.sh
+# Round profile: rocprofv3 kernel trace + stats of the bench command for each config
+# (timed window = the last --steps dispatches of the dominant kernel), then PMC passes
+# (one counter group per run, --kernel-trace only beside --pmc): FETCH_SIZE, WRITE_SIZE,
+# and the SQ instruction counters.
+# Usage: OUT=gpurun_out/prof_rNN bash tools/profile_round.sh [config ...]
 set -o pipefail
 OUT=${OUT:-gpurun_out/prof}
 R=$(pwd)
 mkdir -p "$OUT"
-run() {  # name, timeout, cmd...
-  local name=$1 t=$2; shift 2
-  timeout -k 10 "$t" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"; local rc=$?
-  [ $rc -eq 0 ] || { echo "STEP $name failed rc=$rc"; tail -5 "$OUT/$name.err"; exit 1; }
-}
+CONFIGS=${*:-fixed32 csr fixed4096 fixed32_1g}
 prof() {  # name, args for bench.py
   local name=$1; shift
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
      -d "$R/$OUT/$name" -o run -- python3 "$R/bench.py" "$@" > "$R/$OUT/$name.log" 2>&1) || { echo "PROF $name failed"; tail -5 "$R/$OUT/$name.log"; exit 1; }
-  for c in FETCH_SIZE WRITE_SIZE; do
-    (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --pmc $c --output-format csv \
-       -d "$R/$OUT/${name}_$c" -o pmc -- python3 "$R/bench.py" "$@" > "$R/$OUT/${name}_$c.log" 2>&1) || { echo "PMC $name $c failed"; tail -5 "$R/$OUT/${name}_$c.log"; exit 1; }
+  grep '^{' "$R/$OUT/$name.log" > "$R/$OUT/bench_$name.out" || true
+  local short="--steps 5 --warmup 1 --warm-ms 1 --no-verify"
+  local i=0
+  for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+    i=$((i+1))
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex fnv_ \
+       --output-format csv -d "$R/$OUT/${name}_pmc$i" -o pmc -- python3 "$R/bench.py" "$@" $short > "$R/$OUT/${name}_pmc$i.log" 2>&1) \
+       || { echo "PMC $name pass $i ($c) failed"; tail -5 "$R/$OUT/${name}_pmc$i.log"; exit 1; }
   done
 }
-run bench_fixed32 400 python3 bench.py
-cat "$OUT/bench_fixed32.out"
-run bench_csr 400 python3 bench.py --config csr --steps 10 --warmup 3 --no-cpu-baseline
-cat "$OUT/bench_csr.out"
-run bench_fixed4096 400 python3 bench.py --config fixed4096 --steps 10 --warmup 3 --no-cpu-baseline
-cat "$OUT/bench_fixed4096.out"
-prof fixed32 --steps 10 --warmup 3 --no-cpu-baseline
-prof csr --config csr --steps 5 --warmup 2 --no-cpu-baseline
-prof fixed4096 --config fixed4096 --steps 5 --warmup 2 --no-cpu-baseline
+for cfg in $CONFIGS; do
+  case $cfg in
+    fixed32) prof fixed32 --no-secondary --no-cpu-baseline ;;
+    *) prof "$cfg" --config "$cfg" --steps 20 --warmup 3 --no-cpu-baseline ;;
+  esac
+  echo "profiled $cfg"
+done
 echo PROFILE_ROUND_OK
