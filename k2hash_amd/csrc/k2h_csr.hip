@@ -25,6 +25,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "k2h_fnv_device.h"
 #include "k2h_kernels.h"
 
@@ -325,7 +327,8 @@ __device__ __forceinline__ uint32_t len_bin(uint64_t len) {
 enum {
   kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
   kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10,
-  kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13, kModeLean2Group = 14
+  kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13, kModeLean2Group = 14,
+  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -335,23 +338,23 @@ enum {
     if (tid == 0) prof[(uint64_t)blockIdx.x * 16u + (SLOT)] = __builtin_amdgcn_s_memrealtime(); \
   }
 
-template <bool H2, int MODE, bool EPI>
+template <bool H2, int MODE, bool EPI, int TK = kTileKeys>
 __device__ __forceinline__ void csr_tile(uint64_t tile, const uint8_t* __restrict__ bytes,
                                          const uint64_t* __restrict__ offsets, uint64_t n, const SpadTable& spad_tab,
                                          uint64_t* __restrict__ h1, uint64_t* __restrict__ h2, const BucketParams& bp) {
-  __shared__ uint64_t s_off[kTileKeys + 1];
-  __shared__ uint16_t s_order[kTileKeys];
+  __shared__ uint64_t s_off[TK + 1];
+  __shared__ uint16_t s_order[TK];
   __shared__ uint32_t s_hist[kBins];
   __shared__ uint32_t s_wsum[4];
   __shared__ uint64_t s_spad[16];
   __shared__ TileLds s_u;
 
   const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
-  const uint64_t t0 = tile * kTileKeys;
+  const uint64_t t0 = tile * TK;
   uint64_t* const prof = h2;  // profiling mode only: h2 is the stamp buffer (16 per block)
   (void)prof;
   K2H_PROF_STAMP(0)
-  const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)kTileKeys ? n - t0 : (uint64_t)kTileKeys);
+  const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
   const uint8_t* lo_bound = bytes + offsets[0];
   const uint64_t safe = (uint64_t)(uintptr_t)lo_bound & ~127ull;
 
@@ -382,9 +385,9 @@ __device__ __forceinline__ void csr_tile(uint64_t tile, const uint8_t* __restric
 
   K2H_PROF_STAMP(10)
   // 1. histogram of length classes
-  uint32_t bins[kTileKeys / 256];
+  uint32_t bins[TK / 256];
 #pragma unroll
-  for (int j = 0; j < kTileKeys / 256; ++j) {
+  for (int j = 0; j < TK / 256; ++j) {
     uint32_t k = tid + 256u * j;
     if (k < cnt) {
       bins[j] = len_bin(s_off[k + 1] - s_off[k]);
@@ -409,7 +412,7 @@ __device__ __forceinline__ void csr_tile(uint64_t tile, const uint8_t* __restric
   K2H_PROF_STAMP(12)
   // 3. scatter key indices in class order
 #pragma unroll
-  for (int j = 0; j < kTileKeys / 256; ++j) {
+  for (int j = 0; j < TK / 256; ++j) {
     uint32_t k = tid + 256u * j;
     if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
   }
@@ -474,7 +477,7 @@ __global__ __launch_bounds__(256) void fnv_csr_tile_kernel(const uint8_t* __rest
 // The tiles listed by the lean kernel as too large for its stage (tile_list[0 ..
 // *tile_count)), each hashed with the line ring; a grid-stride loop, since the count is
 // only known on the device.
-template <bool H2, bool EPI = false>
+template <bool H2, bool EPI = false, int TK = kTileKeys>
 __global__ __launch_bounds__(256) void fnv_csr_ring_list_kernel(const uint8_t* __restrict__ bytes,
                                                                 const uint64_t* __restrict__ offsets, uint64_t n,
                                                                 SpadTable spad_tab, uint64_t* __restrict__ h1,
@@ -484,7 +487,7 @@ __global__ __launch_bounds__(256) void fnv_csr_ring_list_kernel(const uint8_t* _
                                                                 BucketParams bp = {}) {
   const uint32_t count = *tile_count;
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
-    csr_tile<H2, kModeRing, EPI>(tile_list[li], bytes, offsets, n, spad_tab, h1, h2, bp);
+    csr_tile<H2, kModeRing, EPI, TK>(tile_list[li], bytes, offsets, n, spad_tab, h1, h2, bp);
     __syncthreads();  // the next tile reuses the shared arrays
   }
 }
@@ -790,6 +793,67 @@ __device__ __forceinline__ void pair_walk(uint32_t k0, uint32_t p0, const uint8_
   }
 }
 
+// Uniform-trip pair walk (round 2).  Every lane runs tmax = max over the wave of k0 + k1
+// chunk steps; chunk t of the lane's sequence (key 0's chunks, then key 1's) is read at
+// base + 16 t, the next one in flight under the current one's hash, the chunk registers
+// alternating between the two asm banks.  One compare per step against the lane's next
+// event -- the end of key 0 (save it, restart from key 1's S_p with its masked chunk 0)
+// or the end of key 1 (save it) -- in a branch only the lanes at that event take.  Lanes
+// past their end re-read the stage start (results dropped).  Outside the hash: the address
+// add and the compare per chunk, and the zero half of the mad64 addend pair stays in v50
+// across the loop (pair_walk: ~5 VALU per chunk and an exec-mask dance per step).
+__device__ __forceinline__ void pair_walk2(uint32_t k0, uint32_t p0, const uint8_t* cp0, uint32_t k1, uint32_t p1,
+                                           const uint8_t* cp1, const uint8_t* safe, const uint64_t* spad,
+                                           const uint4* masks, uint64_t& h0, uint64_t& h1v) {
+  const uint32_t T = k0 + k1;
+  const uint32_t tmax = __builtin_amdgcn_readfirstlane(wave_max(T));
+  h0 = 0;
+  h1v = 0;
+  if (tmax == 0) return;
+  uint64_t st = spad[p0];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), z = 0;
+  const uint8_t* base = T ? cp0 : safe;
+  uint32_t ev = T ? k0 : 0xFFFFFFFFu;  // next event: end of key 0, then of key 1
+  bool second = false;
+  uint4 m = masks[p0];
+  uint4 a = ld16(base);
+  a = make_uint4(a.x & m.x, a.y & m.y, a.z & m.z, a.w & m.w);
+  uint4 b;
+  // at the end of a key (state = its hash): save it, then restart on key 1 (c becomes its
+  // masked chunk 0, read from cp1) or retire the lane
+  auto event = [&](uint32_t t, uint4& c) {
+    if (!second) {
+      h0 = ((uint64_t)hi << 32) | lo;
+      if (k1) {
+        second = true;
+        st = spad[p1];
+        lo = (uint32_t)st;
+        hi = (uint32_t)(st >> 32);
+        base = cp1 - 16 * (int32_t)t;
+        m = masks[p1];
+        c = ld16(cp1);
+        c = make_uint4(c.x & m.x, c.y & m.y, c.z & m.z, c.w & m.w);
+        ev = T;
+        return;
+      }
+    } else {
+      h1v = ((uint64_t)hi << 32) | lo;
+    }
+    ev = 0xFFFFFFFFu;
+    base = safe - 16 * (int32_t)t;
+  };
+  for (uint32_t t = 0;; t += 2) {
+    b = ld16(base + 16u * (t + 1));
+    fnv_chunk16z<0>(lo, hi, a, z);
+    if (t + 1 == ev) event(t + 1, b);
+    if (t + 1 >= tmax) break;
+    a = ld16(base + 16u * (t + 2));
+    fnv_chunk16z<1>(lo, hi, b, z);
+    if (t + 2 == ev) event(t + 2, a);
+    if (t + 2 >= tmax) break;
+  }
+}
+
 template <bool H2, bool EPI = false, int WALK = 0>
 __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
@@ -927,6 +991,177 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
       if constexpr (H2) h2[t0 + k] = r2;
       if constexpr (EPI) bucket_emit<false>(bp, t0 + k, r1);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CSR pair tiles (round 2): TK = 128 NW keys per tile, NW waves, lane i of the block hashes
+// sorted keys i and TK-1-i back to back (pair_walk), the tile's bytes DMA'd into a
+// STAGE_KIB KiB LDS stage.  Compared with fnv_csr_lean2_kernel (512 keys, 4 waves, 72 KiB,
+// two blocks per CU):
+//  - smaller tiles fit more independent blocks per CU (NW = 2: 256 keys, 36 KiB, four
+//    blocks), so the blocks of a CU drift out of phase and one block's load / sort phase
+//    overlaps the others' hashing instead of all of them loading, then all hashing;
+//  - PERSIST: a grid of resident blocks walks the tiles with a stride, and each block
+//    loads the offsets of its next tile into registers before it starts hashing the
+//    current one, so the next tile starts without a round trip to HBM (1.6 us of a
+//    10.3 us tile life in round 1, profiles/r01f_csr_phases_sortfix.txt).
+// Tiles whose span exceeds the stage are listed for the ring kernel, as in lean2.
+// ---------------------------------------------------------------------------
+template <bool H2, bool EPI, int NW, int STAGE_KIB, bool PERSIST>
+__global__ __launch_bounds__(NW * 64) void fnv_csr_pair_kernel(const uint8_t* __restrict__ bytes,
+                                                               const uint64_t* __restrict__ offsets, uint64_t n,
+                                                               SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                               uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
+                                                               uint32_t* __restrict__ over_count, BucketParams bp = {}) {
+  constexpr uint32_t NT = NW * 64, TK = 2 * NT, NB = 128;
+  constexpr uint32_t kStage = STAGE_KIB * 1024u;
+  static_assert(NT >= NB || NB % NT == 0, "scan covers the length classes");
+  __shared__ uint32_t s_rel[TK + 1];
+  __shared__ uint16_t s_order[TK];
+  __shared__ uint32_t s_hist[NB];
+  __shared__ uint32_t s_wsum[NW];
+  __shared__ uint64_t s_spad[16];
+  __shared__ uint4 s_mask[16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[16 + kStage];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t ntiles = (n + TK - 1) / TK;
+  uint64_t tile = blockIdx.x;
+  if (tid < 16) {
+    s_spad[tid] = spad_tab.v[tid];
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
+      int32_t sh = 8 * ((int32_t)tid - 4 * i);
+      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
+    }
+    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  // this thread's offsets of a tile: keys tid and tid + NT, and the tile's first / end offset
+  // (the same address in every lane: loaded per lane through an index the compiler cannot
+  // see is zero, so they are vector loads and not scalar loads, whose out-of-order return
+  // would make every LDS wait of the hash loop a full lgkmcnt(0) until they land)
+  // (a and b: only the low words -- the tile-relative offsets are 32-bit -- so no half of a
+  // pending load's destination is dead and reused, which would force a wait for it)
+  const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
+  auto fetch = [&](uint64_t t, uint32_t& a, uint32_t& b, uint64_t& z, uint64_t& e) {
+    const uint64_t t0 = t * TK;
+    const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
+    uint32_t zero = 0;
+    asm volatile("" : "+v"(zero));
+    a = off32[2 * (t0 + (tid < cnt ? tid : cnt))];
+    b = off32[2 * (t0 + (tid + NT < cnt ? tid + NT : cnt))];
+    z = offsets[t0 + zero];
+    e = offsets[t0 + cnt + zero];
+  };
+  uint32_t pa, pb;
+  uint64_t pz, pe;
+  fetch(tile, pa, pb, pz, pe);
+  for (;;) {
+    const uint64_t t0 = tile * TK;
+    const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
+    const uint64_t o0 = pz, oN = pe;  // block-uniform
+    const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
+    const uint64_t span_lo = kb & ~15ull;
+    const uint32_t delta = (uint32_t)(kb & 15u);
+    const uint64_t span = oN - o0 + delta;  // stage bytes up to the tile's last key byte
+    const uint64_t next = tile + gridDim.x;
+    if (span > kStage) {  // block-uniform: the ring kernel hashes this tile
+      if (tid == 0) over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
+      if (!PERSIST || next >= ntiles) return;
+      tile = next;
+      fetch(tile, pa, pb, pz, pe);
+      continue;
+    }
+    if (tid < cnt) s_rel[tid] = pa - (uint32_t)o0;
+    if (tid + NT < cnt) s_rel[tid + NT] = pb - (uint32_t)o0;
+    if (tid == 0) s_rel[cnt] = (uint32_t)(oN - o0);
+    if (tid < NB) s_hist[tid] = 0;
+    // DMA of the tile span (16-byte pieces; pieces past the span re-read its last piece
+    // into stage bytes nobody reads), in flight during the sort
+    if (oN > o0) {
+      const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
+      const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
+      const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
+      uint32_t off = 1024u * wave + 16u * lane;
+      for (uint32_t c = wave; c < npieces; c += NW, off += 1024u * NW) {
+        const uint32_t o = off < lastp ? off : lastp;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
+                                         (__attribute__((address_space(3))) void*)(s_stage + 16 + 1024u * c), 16, 0, 0);
+      }
+    }
+    lds_barrier();
+    uint32_t bins[2];
+#pragma unroll
+    for (uint32_t j = 0; j < 2; ++j) {
+      const uint32_t k = tid + NT * j;
+      if (k < cnt) {
+        bins[j] = len_bin128_32(s_rel[k + 1] - s_rel[k]);
+        lds_add(&s_hist[bins[j]], 1u);
+      }
+    }
+    lds_barrier();
+    // exclusive scan of the 128 class counts
+    uint32_t v = tid < NB ? s_hist[tid] : 0u, incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    lds_barrier();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
+    if (tid < NB) s_hist[tid] = base + incl - v;
+    lds_barrier();
+#pragma unroll
+    for (uint32_t j = 0; j < 2; ++j) {
+      const uint32_t k = tid + NT * j;
+      if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces have landed
+    lds_barrier();                                     // ... and every wave's
+    // The next tile's offsets, in flight while this one is hashed (PERSIST).  Issued after a
+    // first read of the stage: the compiler puts its own vmcnt(0) for the DMA'd object in
+    // front of that read, and must not put it after the prefetch (it would wait for it).
+    const bool more = PERSIST && next < ntiles;
+    if constexpr (PERSIST) {
+      const uint32_t touch = s_stage[16];
+      asm volatile("" ::"v"(touch) : "memory");
+      fetch(more ? next : tile, pa, pb, pz, pe);  // unconditional: no phi copies that would wait for it
+    }
+    const uint8_t* key0 = s_stage + 16 + delta;
+    {
+      const uint32_t i = tid;
+      const bool has_a = i < (cnt + 1u) / 2u, has_b = i < cnt / 2u;
+      const uint32_t ka = s_order[has_a ? i : 0u], kbi = s_order[has_b ? cnt - 1u - i : 0u];
+      const uint32_t ra = s_rel[ka], rae = s_rel[ka + 1], rb = s_rel[kbi], rbe = s_rel[kbi + 1];
+      const uint32_t la = has_a ? rae - ra : 0u, lb = has_b ? rbe - rb : 0u;
+      const uint32_t kA = (la + 15u) >> 4, kB = (lb + 15u) >> 4;
+      const uint32_t pA = (0u - la) & 15u, pB = (0u - lb) & 15u;
+      const uint8_t* cpA = key0 + (int32_t)(rae - 16u * kA);
+      const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
+      const bool only_b = kA == 0;  // key A empty (or absent): walk B alone
+      uint64_t hw0, hw1;
+      pair_walk2(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
+                 s_spad, s_mask, hw0, hw1);
+      const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
+      if (has_a) {
+        h1[t0 + ka] = hA;
+        if constexpr (H2) h2[t0 + ka] = second_from_first(hA, la, key0 + rae);
+        if constexpr (EPI) bucket_emit<false>(bp, t0 + ka, hA);
+      }
+      if (has_b) {
+        h1[t0 + kbi] = hB;
+        if constexpr (H2) h2[t0 + kbi] = second_from_first(hB, lb, key0 + rbe);
+        if constexpr (EPI) bucket_emit<false>(bp, t0 + kbi, hB);
+      }
+    }
+    if (!more) return;
+    tile = next;
+    lds_barrier();  // every lane is done with the stage and the sort arrays
   }
 }
 
@@ -1091,10 +1326,70 @@ static hipError_t launch_lean2(const uint8_t* b, const uint64_t* offsets, uint64
   return hipGetLastError();
 }
 
+// Resident blocks of a kernel per device (occupancy x CUs), computed once per device and
+// kernel; safe to call from any thread.
+template <typename K>
+static unsigned resident_grid(K kernel, int threads, unsigned cap) {
+  constexpr int kMaxDev = 64;
+  static std::atomic<unsigned> cache[kMaxDev];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
+  unsigned g = cache[dev].load(std::memory_order_relaxed);
+  if (!g) {
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kernel, threads, 0) != hipSuccess ||
+        per_cu <= 0)
+      per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+    g = (unsigned)(per_cu * cus);
+    cache[dev].store(g, std::memory_order_relaxed);
+  }
+  return g < cap ? g : cap;
+}
+
+// pair-tile kernel (TK = 128 NW keys) + the ring pass over its oversize-tile list
+template <int NW, int KIB, bool PERSIST>
+static hipError_t launch_pair(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
+                              uint64_t* h2, const BucketParams* bp, hipStream_t stream) {
+  constexpr uint64_t TK = 128 * NW;
+  const uint64_t ntiles = (n + TK - 1) / TK;
+  if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  uint32_t* scratch = nullptr;  // [0] = count, [1..] = tile list
+  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (ntiles + 1), stream);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(scratch, 0, 4, stream);
+  const BucketParams none{};
+  const BucketParams& p = bp ? *bp : none;
+  const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
+#define K2H_PAIR(H2, EPI)                                                                                        \
+  {                                                                                                            \
+    auto k = fnv_csr_pair_kernel<H2, EPI, NW, KIB, PERSIST>;                                                   \
+    const unsigned g = PERSIST ? resident_grid(k, NW * 64, (unsigned)ntiles) : (unsigned)ntiles;               \
+    k<<<g, NW * 64, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, scratch + 1, scratch, p);            \
+    fnv_csr_ring_list_kernel<H2, EPI, (int)TK><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, \
+                                                                       scratch + 1, scratch, p);               \
+  }
+  if (e == hipSuccess) {
+    if (bp) {
+      if (h2) K2H_PAIR(true, true) else K2H_PAIR(false, true)
+    } else {
+      if (h2) K2H_PAIR(true, false) else K2H_PAIR(false, false)
+    }
+    e = hipGetLastError();
+  }
+#undef K2H_PAIR
+  hipError_t f = hipFreeAsync(scratch, stream);
+  return e != hipSuccess ? e : f;
+}
+
 #if K2H_AMD_LAB
 static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
   SpadTable t = make_spad(seed);
+  if (mode == kModePair2) return launch_pair<2, 36, false>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModePair2P) return launch_pair<2, 36, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModePair4P) return launch_pair<4, 72, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModePair4) return launch_pair<4, 72, false>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
   const uint8_t* b = (const uint8_t*)bytes;
   if (mode == kModeLeanRing || mode == kModeLean2Ring || mode == kModeLean2Pin || mode == kModeLean2Step ||

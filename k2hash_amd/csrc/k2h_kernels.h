@@ -82,6 +82,10 @@ enum {
   kVariantRalleBatch2 = 58,
   kVariantFixed32Pipe64 = 59,     // fixed32: persistent, next tile's loads issued before hashing the current
   kVariantFixed32Pipe256 = 60,    // (one-wave / 256-thread blocks, two keys per lane)
+  kVariantCsrPair2 = 61,          // csr pair tiles: 256 keys, 2 waves, 36 KiB stage (4 blocks per CU)
+  kVariantCsrPair2P = 62,         // ... persistent blocks, next tile's offsets prefetched during the hash
+  kVariantCsrPair4P = 63,         // ... 512 keys, 4 waves, 72 KiB, persistent
+  kVariantCsrPair4 = 64,          // ... 512 keys, 4 waves, 72 KiB
 };
 #endif
 

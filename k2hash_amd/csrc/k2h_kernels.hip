@@ -792,6 +792,10 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrLean2Pin ? 12
                          : variant == kVariantCsrLean2Step ? 13
                          : variant == kVariantCsrLean2Group ? 14
+                         : variant == kVariantCsrPair2 ? 15
+                         : variant == kVariantCsrPair2P ? 16
+                         : variant == kVariantCsrPair4P ? 17
+                         : variant == kVariantCsrPair4 ? 18
                                                         : 11,
                          stream, epi ? bp : nullptr);
 }

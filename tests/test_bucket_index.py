@@ -53,6 +53,43 @@ def test_linetool_dsave_fixture_pin(oracle):
     assert reach and min(reach) >= 3
 
 
+def _ki_array_count(area: int) -> int:
+    """KIArrayCount of key_index_area[area]: the table at lib/k2hshm.cc:800-808 lists
+    area 0 -> PKINDEX[1], 1 -> [1], 2 -> [2], 3 -> [4]: 2^(area-1) from area 1 on.  (Its last
+    two rows, 0x7FFFFFFF -> area 30 and 0xFFFFFFFF -> area 31, are one lower than
+    GetKIndexPos's loop at :822-826 gives for 31- and 32-bit masks; the loop is what runs,
+    so the rule of the first rows is extended.)"""
+    return 1 if area == 0 else 1 << (area - 1)
+
+
+@pytest.mark.parametrize("cmask", [0x0, 0x3, 0xF, (1 << 12) - 1])
+def test_key_index_area_table_pin(oracle, cmask):
+    """Second pin of the restatement: the reference's own key_index_area table
+    (lib/k2hshm.cc:800-808).  For every cur_mask of the form 2^m - 1 the table admits:
+    KIPtrArrayPos <= m; KIArrayPos < KIArrayCount(KIPtrArrayPos); and -- checked
+    exhaustively over every shifted hash below 2^m for m <= 12 -- area p (p >= 1) is hit
+    by exactly KIArrayCount(p) distinct KIArrayPos, area 0 by one, so the table's counts
+    are exactly the index space GetKIndexPos addresses."""
+    cshift = int(cmask).bit_length()
+    rng = np.random.default_rng(cmask)
+    for m in range(0, 33):
+        cur = (1 << m) - 1
+        hs = rng.integers(0, 2**63, 2000, dtype=np.int64).view(np.uint64) * np.uint64(5)
+        hs[:3] = [0, 0xFFFFFFFFFFFFFFFF, np.uint64(cur) << np.uint64(cshift)]
+        k, _ = oracle.bucket_index(hs, cur, cmask)
+        pos, arr = batch.unpack_kindex(k)
+        assert int(pos.max()) <= m
+        assert int(pos[1]) == m and int(pos[2]) == m  # all mask bits set -> the table's last area
+        assert all(int(a) < _ki_array_count(int(p)) for p, a in zip(pos, arr))
+        if m <= 12:
+            every = (np.arange(1 << m, dtype=np.uint64) << np.uint64(cshift)) | np.uint64(cmask & 0x5)
+            k, _ = oracle.bucket_index(every, cur, cmask)
+            pos, arr = batch.unpack_kindex(k)
+            for area in range(0, m + 1):
+                hit = {int(a) for p, a in zip(pos, arr) if int(p) == area}
+                assert len(hit) == _ki_array_count(area), (m, area)
+
+
 def test_kindex_packing_helpers():
     kv = np.array([(8 << 58) | 0x54, 0, (58 << 58) | ((1 << 58) - 1)], np.uint64)
     pos, arr = batch.unpack_kindex(kv)
@@ -127,14 +164,25 @@ def test_fused_csr_vs_oracle(cuda, oracle):
 
 
 @pytest.mark.gpu
-def test_fused_full_size_matches_standalone(cuda, oracle, digests):
-    """Config 2 at full size: the fused epilogue equals the standalone one over the
-    kernel's own h1, whose digest is the reference's."""
+@pytest.mark.parametrize("cfgname,cur,cm", [("fixed32_16M", 0xFF, 0xF), ("fixed32_16M", (1 << 28) - 1, 0xF),
+                                             ("csr_8_256_64M", (1 << 24) - 1, 0x3F)])
+def test_fused_full_size_vs_oracle(cuda, oracle, digests, cfgname, cur, cm):
+    """Configs 2 and 3 at full size: h1 from the fused kernel matches the reference's digest
+    (so it IS the reference's h1, key for key up to digest collisions), and the fused kindex /
+    ckindex equal the oracle's restatement applied to that h1 -- not a self-comparison with
+    the standalone kernel."""
     import torch
-    cfg = digests["fixed32_16M"]
-    keys = batch.synth_bytes(cfg["n"] * 32, cuda)
-    h1, _, k, c = k2hash_amd.hash_fixed_index(keys, 32, 0xFF, 0xF)
-    k2, c2 = k2hash_amd.bucket_index(h1, 0xFF, 0xF)
+    cfg = digests[cfgname]
+    if cfg["kind"] == "fixed":
+        keys = batch.synth_bytes(cfg["n"] * cfg["key_len"], cuda)
+        h1, _, k, c = k2hash_amd.hash_fixed_index(keys, cfg["key_len"], cur, cm)
+    else:
+        off = batch.synth_offsets(cfg["n"], cuda, cfg["min_len"], cfg["max_len"])
+        keys = batch.synth_bytes(int(off[-1].item()), cuda)
+        h1, _, k, c = k2hash_amd.hash_csr_index(keys, off, cur, cm)
     torch.cuda.synchronize()
-    assert [f"{x:016x}" for x in oracle.digest(h1.cpu().numpy().view(np.uint64))] == cfg["h1"]
-    assert torch.equal(k, k2) and torch.equal(c, c2)
+    hh = h1.cpu().numpy().view(np.uint64)
+    assert [f"{x:016x}" for x in oracle.digest(hh)] == cfg["h1"]
+    rk, rc = oracle.bucket_index(hh, cur, cm)
+    assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
+    assert np.array_equal(c.cpu().numpy().view(np.uint64), rc)

@@ -212,11 +212,12 @@ def test_full_size_csr_digest(cuda, oracle, digests, name):
 
 
 def test_config4_shard_digests(cuda, oracle, digests):
-    """Config 4 (1 B x 32 B over 8 GPUs): each rank's shard, hashed here one at a time,
-    matches the reference's digest of that shard."""
+    """Config 4 (1 B x 32 B over 8 GPUs): each of the eight ranks' shards, hashed here one at
+    a time, matches the reference's digest of that shard."""
     import torch
     cfg = digests["fixed32_1G"]
-    for c in cfg["chunks"][:2]:
+    assert len(cfg["chunks"]) == 8
+    for c in cfg["chunks"]:
         keys = batch.synth_bytes(c["count"] * 32, cuda, byte_off=c["first"] * 32)
         h1, h2 = k2hash_amd.hash_fixed(keys, 32, second=True)
         torch.cuda.synchronize()
