@@ -86,6 +86,7 @@ enum {
   kVariantCsrPair2P = 62,         // ... persistent blocks, next tile's offsets prefetched during the hash
   kVariantCsrPair4P = 63,         // ... 512 keys, 4 waves, 72 KiB, persistent
   kVariantCsrPair4 = 64,          // ... 512 keys, 4 waves, 72 KiB
+  kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };
 #endif
 

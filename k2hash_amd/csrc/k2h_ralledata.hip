@@ -134,6 +134,96 @@ __global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, ui
 }
 
 #if K2H_AMD_LAB
+// Staged form (round-2 A/B variant 65, measured SLOWER: 2.14 vs 1.50 ms on 8M records --
+// the LDS round trip and the block barrier cost more than the unaligned HBM stores): a block assembles the blobs of RPB consecutive records in
+// an LDS image of their packed output span -- headers and segment pieces written at their
+// (unaligned) blob positions, as the group form writes them to HBM -- then stores the span
+// as aligned 16-byte pieces, consecutive lanes on consecutive pieces, i.e. whole 128-byte
+// lines; only the two pieces a block shares with its neighbours are written byte by byte.
+// The group form's unaligned 16-byte stores straight to HBM ran at ~2.3 TB/s.  A block
+// whose span exceeds the image (records far larger than BASELINE-like ones) assembles
+// straight to HBM like the group form.
+template <int G>
+__device__ __forceinline__ void group_copy_lds(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                               uint64_t len, uint32_t q) {
+  const uint64_t full = len & ~15ull;
+  for (uint64_t j = 16ull * q; j < full; j += 16ull * G)
+    *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
+  if (full == len) return;
+  if (len >= 16) {
+    if (q == G - 1) *reinterpret_cast<u32x4_ua*>(dst + len - 16) = *reinterpret_cast<const u32x4_ua*>(src + len - 16);
+    return;
+  }
+  for (uint64_t t = q; t < len; t += G) dst[t] = src[t];
+}
+
+__device__ __forceinline__ uint64_t blob_start(const RalleInputs& in, uint64_t i) {
+  return 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) + seg_before(in.aoff, i);
+}
+
+template <int RPB, int IMG>
+__global__ __launch_bounds__(256) void ralledata_stage_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
+                                                              uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
+  constexpr int G = 8, NG = 256 / G;
+  __shared__ __attribute__((aligned(16))) uint8_t img[IMG];
+  const uint32_t tid = threadIdx.x, q = tid % G, grp = tid / G;
+  const uint64_t r0 = (uint64_t)blockIdx.x * RPB;
+  const uint32_t nr = (uint32_t)(n - r0 < (uint64_t)RPB ? n - r0 : (uint64_t)RPB);
+  const uint64_t o_first = blob_start(in, r0), o_end = blob_start(in, r0 + nr);
+  const uint64_t a0 = o_first & ~15ull;
+  const bool staged = o_end - a0 <= (uint64_t)IMG;  // block-uniform
+  // one record's blob at b (LDS image or HBM: two inlined copies, so each writes through its
+  // own address space instead of flat stores)
+  auto assemble = [&](uint8_t* __restrict__ b, uint64_t i, uint64_t kl, uint64_t vl, uint64_t sl, uint64_t al) {
+    if (q < 5) {
+      uint64_t f0, f1;
+      switch (q) {
+        case 0: f0 = h[i]; f1 = h[n + i]; break;
+        case 1: f0 = kl; f1 = vl; break;
+        case 2: f0 = sl; f1 = al; break;
+        case 3: f0 = 80; f1 = 80 + kl; break;
+        default: f0 = 80 + kl + vl; f1 = 80 + kl + vl + sl; break;
+      }
+      *reinterpret_cast<u32x4_ua*>(b + 16 * q) =
+          u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
+    }
+    if (kl) group_copy_lds<G>(b + 80, in.keys + in.koff[i], kl, q);
+    if (vl) group_copy_lds<G>(b + 80 + kl, in.vals + in.voff[i], vl, q);
+    if (sl) group_copy_lds<G>(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
+    if (al) group_copy_lds<G>(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
+  };
+  for (uint32_t rec = grp; rec < nr; rec += NG) {
+    const uint64_t i = r0 + rec;
+    const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i),
+                   al = seg_len(in.aoff, i);
+    const uint64_t o = blob_start(in, i);
+    if (staged) assemble(img + (uint32_t)(o - a0), i, kl, vl, sl, al);
+    else assemble(out + o, i, kl, vl, sl, al);
+    if (blob_off && q == 0) {
+      blob_off[i] = o;
+      if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
+    }
+  }
+  if (!staged) return;
+  __syncthreads();
+  // pieces [a0 + 16 p, +16); the first and the last may hold a neighbour's bytes
+  const uint32_t np = (uint32_t)((o_end - a0 + 15) >> 4);
+  typedef uint32_t u32x4_al __attribute__((ext_vector_type(4)));
+  for (uint32_t p = tid; p < np; p += 256) {
+    const uint64_t lo = a0 + 16ull * p;
+    if (lo >= o_first && lo + 16 <= o_end) {
+      __builtin_nontemporal_store(*reinterpret_cast<const u32x4_al*>(img + 16 * p),
+                                  reinterpret_cast<u32x4_al*>(out + lo));
+    } else {
+      for (uint32_t j = 0; j < 16; ++j)
+        if (lo + j >= o_first && lo + j < o_end) out[lo + j] = img[16 * p + j];
+    }
+  }
+}
+
+#endif  // K2H_AMD_LAB
+
+#if K2H_AMD_LAB
 // Batched form (A/B variants 57-58, measured slower: 1.56 ms at 2 and 2.13 ms at 4 records
 // per group vs 1.50 for the group form -- the register cost (82 / 152 VGPRs) outweighs the
 // extra loads in flight).  Motivation: a header-only probe of the group form already
@@ -246,6 +336,11 @@ __global__ __launch_bounds__(256) void ralledata_batch_kernel(RalleInputs in, ui
 
 }  // namespace
 
+#if K2H_AMD_LAB
+constexpr int kRalleRecsPerBlock = 64;   // ~16 KB of blobs for BASELINE-like records (80 + 8-64 + 0-256 B)
+constexpr int kRalleImage = 32 * 1024;   // 4 blocks per CU; spans above it assemble straight to HBM
+#endif
+
 hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, uint8_t* out, uint64_t* blob_off,
                             int variant, hipStream_t stream) {
   if (n == 0) {
@@ -272,6 +367,9 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
       ralledata_batch_kernel<8, 4><<<(unsigned)(((n + 3) / 4 * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     else if (variant == kVariantRalleBatch2)
       ralledata_batch_kernel<8, 2><<<(unsigned)(((n + 1) / 2 * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else if (variant == kVariantRalleStage)
+      ralledata_stage_kernel<kRalleRecsPerBlock, kRalleImage>
+          <<<(unsigned)((n + kRalleRecsPerBlock - 1) / kRalleRecsPerBlock), 256, 0, stream>>>(in, n, h, out, blob_off);
     else
 #endif
       ralledata_group_kernel<8><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
