@@ -328,7 +328,7 @@ enum {
   kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
   kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10,
   kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13, kModeLean2Group = 14,
-  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18
+  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -793,7 +793,9 @@ __device__ __forceinline__ void pair_walk(uint32_t k0, uint32_t p0, const uint8_
   }
 }
 
-// Uniform-trip pair walk (round 2).  Every lane runs tmax = max over the wave of k0 + k1
+// Uniform-trip pair walk (round 2; A/B variant 68, measured slower than pair_walk: the end
+// event needs the same branch as the switch, and its state copies cost more VALU than the
+// per-step compares it saves -- SQ_INSTS_VALU 1.026e9 vs 0.994e9).  Every lane runs tmax = max over the wave of k0 + k1
 // chunk steps; chunk t of the lane's sequence (key 0's chunks, then key 1's) is read at
 // base + 16 t, the next one in flight under the current one's hash, the chunk registers
 // alternating between the two asm banks.  One compare per step against the lane's next
@@ -1008,7 +1010,7 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
 //    10.3 us tile life in round 1, profiles/r01f_csr_phases_sortfix.txt).
 // Tiles whose span exceeds the stage are listed for the ring kernel, as in lean2.
 // ---------------------------------------------------------------------------
-template <bool H2, bool EPI, int NW, int STAGE_KIB, bool PERSIST>
+template <bool H2, bool EPI, int NW, int STAGE_KIB, bool PERSIST, bool STAGGER = false, bool W2 = false>
 __global__ __launch_bounds__(NW * 64) void fnv_csr_pair_kernel(const uint8_t* __restrict__ bytes,
                                                                const uint64_t* __restrict__ offsets, uint64_t n,
                                                                SpadTable spad_tab, uint64_t* __restrict__ h1,
@@ -1059,6 +1061,13 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_pair_kernel(const uint8_t* __
   uint32_t pa, pb;
   uint64_t pz, pe;
   fetch(tile, pa, pb, pz, pe);
+  if constexpr (PERSIST && STAGGER) {
+    // resident blocks start in lock step; the second half of the grid (the other blocks of
+    // each CU) starts about half a tile later, so one block's load / sort phase overlaps
+    // its neighbours' hashing instead of coinciding with it
+    if (blockIdx.x >= gridDim.x / 2)
+      for (int i = 0; i < 40; ++i) __builtin_amdgcn_s_sleep(127);
+  }
   for (;;) {
     const uint64_t t0 = tile * TK;
     const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
@@ -1145,8 +1154,12 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_pair_kernel(const uint8_t* __
       const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
       const bool only_b = kA == 0;  // key A empty (or absent): walk B alone
       uint64_t hw0, hw1;
-      pair_walk2(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
-                 s_spad, s_mask, hw0, hw1);
+      if constexpr (W2)
+        pair_walk2(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
+                   s_spad, s_mask, hw0, hw1);
+      else
+        pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
+                  hw0, hw1);
       const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
       if (has_a) {
         h1[t0 + ka] = hA;
@@ -1348,7 +1361,7 @@ static unsigned resident_grid(K kernel, int threads, unsigned cap) {
 }
 
 // pair-tile kernel (TK = 128 NW keys) + the ring pass over its oversize-tile list
-template <int NW, int KIB, bool PERSIST>
+template <int NW, int KIB, bool PERSIST, bool STAGGER = false, bool W2 = false>
 static hipError_t launch_pair(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
                               uint64_t* h2, const BucketParams* bp, hipStream_t stream) {
   constexpr uint64_t TK = 128 * NW;
@@ -1363,7 +1376,7 @@ static hipError_t launch_pair(const uint8_t* b, const uint64_t* offsets, uint64_
   const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
 #define K2H_PAIR(H2, EPI)                                                                                        \
   {                                                                                                            \
-    auto k = fnv_csr_pair_kernel<H2, EPI, NW, KIB, PERSIST>;                                                   \
+    auto k = fnv_csr_pair_kernel<H2, EPI, NW, KIB, PERSIST, STAGGER, W2>;                                                   \
     const unsigned g = PERSIST ? resident_grid(k, NW * 64, (unsigned)ntiles) : (unsigned)ntiles;               \
     k<<<g, NW * 64, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, scratch + 1, scratch, p);            \
     fnv_csr_ring_list_kernel<H2, EPI, (int)TK><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, \
@@ -1390,6 +1403,9 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModePair2P) return launch_pair<2, 36, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair4P) return launch_pair<4, 72, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair4) return launch_pair<4, 72, false>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModePair4W2) return launch_pair<4, 72, false, false, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModePair4PS) return launch_pair<4, 72, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModePair2PS) return launch_pair<2, 36, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
   const uint8_t* b = (const uint8_t*)bytes;
   if (mode == kModeLeanRing || mode == kModeLean2Ring || mode == kModeLean2Pin || mode == kModeLean2Step ||

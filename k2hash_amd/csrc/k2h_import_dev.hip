@@ -319,8 +319,24 @@ __global__ __launch_bounds__(kThreads) void import_hash_kernel(const uint8_t* __
 }
 
 // TSV: record r ends at TAB line rl[r]; its key starts after the previous TAB line.
+// nul_from[k] = the first line j >= nlines - 1 - k whose bytes hold a NUL (kNone if none):
+// a min-scan over the lines in reverse order, so a record whose key spans many TAB-less
+// lines cuts it at its first NUL in O(1) (one lane used to walk those lines).
+struct NulLineRev {
+  const LineInfo* info;
+  uint64_t nlines;
+  __host__ __device__ uint64_t operator()(uint64_t k) const {
+    const uint64_t j = nlines - 1 - k;
+    return info[j].nul != kNone ? j : kNone;
+  }
+};
+struct MinOp {
+  __host__ __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a < b ? a : b; }
+};
+
 __global__ __launch_bounds__(kThreads) void tsv_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
                                                                uint64_t size, const LineInfo* __restrict__ info,
+                                                               const uint64_t* __restrict__ nul_from, uint64_t nlines,
                                                                const uint64_t* __restrict__ rl, uint64_t nrec,
                                                                k2h_amd_import_rec* __restrict__ recs,
                                                                const uint8_t* __restrict__ f, SpadTable sp,
@@ -331,11 +347,10 @@ __global__ __launch_bounds__(kThreads) void tsv_records_kernel(const uint64_t* _
   const uint64_t kb = line_begin(nl, j0);
   const LineInfo L = info[j1];
   uint64_t kend = L.tab;
-  for (uint64_t j = j0; j < j1; ++j)  // key lines before the TAB line (usually none)
-    if (info[j].nul != kNone) {
-      kend = info[j].nul;
-      break;
-    }
+  if (j1 > j0) {  // key lines before the TAB line (usually none): the first NUL in them, O(1)
+    const uint64_t jn = nul_from[nlines - 1 - j0];  // first line >= j0 holding a NUL
+    if (jn < j1) kend = info[jn].nul;
+  }
   if (kend == L.tab && L.nul != kNone && L.nul < L.tab) kend = L.nul;
   const uint64_t vb = L.tab + 1, ve = L.nul_tab != kNone ? L.nul_tab : line_end(nl, nnl, size, j1);
   k2h_amd_import_rec o;
@@ -521,11 +536,23 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
       }
     }
   }
+  uint64_t* nul_from = nullptr;
+  void* tmp2 = nullptr;
   if (e == hipSuccess && tsv) {
     if (recs && nrec && nrec <= cap) {
-      tsv_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, rl, nrec, recs, f,
-                                                                    make_spad(seed), h1, h2);
-      e = hipGetLastError();
+      hipcub::CountingInputIterator<uint64_t> idx(0);
+      hipcub::TransformInputIterator<uint64_t, NulLineRev, hipcub::CountingInputIterator<uint64_t>> nul_rev(
+          idx, NulLineRev{info, nlines});
+      size_t t3 = 0;
+      K2H_TRY(scratch_alloc((void**)&nul_from, nlines * 8, stream));
+      K2H_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, t3, nul_rev, nul_from, MinOp(), nlines, stream));
+      K2H_TRY(scratch_alloc(&tmp2, t3 ? t3 : 1, stream));
+      K2H_TRY(hipcub::DeviceScan::InclusiveScan(tmp2, t3, nul_rev, nul_from, MinOp(), nlines, stream));
+      if (e == hipSuccess) {
+        tsv_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, nul_from, nlines, rl, nrec,
+                                                                      recs, f, make_spad(seed), h1, h2);
+        e = hipGetLastError();
+      }
     }
   } else if (e == hipSuccess && format == K2H_AMD_IMPORT_MDBM) {
     // header: five getline calls; the fifth must extract exactly "HEADER=END"
@@ -559,7 +586,7 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   K2H_TRY(hipStreamSynchronize(stream));
 #undef K2H_TRY
   for (void* p : {(void*)bcnt, (void*)bbase, (void*)bst, (void*)bin, (void*)brec2, (void*)brec, (void*)rbase, (void*)nl,
-                  (void*)rl, (void*)info, tmp})
+                  (void*)rl, (void*)info, tmp, (void*)nul_from, tmp2})
     if (p) (void)hipFreeAsync(p, stream);
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;

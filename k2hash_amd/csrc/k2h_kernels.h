@@ -86,6 +86,9 @@ enum {
   kVariantCsrPair2P = 62,         // ... persistent blocks, next tile's offsets prefetched during the hash
   kVariantCsrPair4P = 63,         // ... 512 keys, 4 waves, 72 KiB, persistent
   kVariantCsrPair4 = 64,          // ... 512 keys, 4 waves, 72 KiB
+  kVariantCsrPair4PS = 66,        // csr pair tiles, persistent, second half of the grid starts half a tile late
+  kVariantCsrPair2PS = 67,
+  kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };
 #endif

@@ -796,6 +796,9 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrPair2P ? 16
                          : variant == kVariantCsrPair4P ? 17
                          : variant == kVariantCsrPair4 ? 18
+                         : variant == kVariantCsrPair4PS ? 19
+                         : variant == kVariantCsrPair2PS ? 20
+                         : variant == kVariantCsrPair4W2 ? 21
                                                         : 11,
                          stream, epi ? bp : nullptr);
 }

@@ -216,3 +216,19 @@ def test_device_scan_and_prehash_large(cuda):
     frecs, f1, f2 = archive.import_scan_prehash_device(f)
     torch.cuda.synchronize()
     assert torch.equal(frecs, recs) and torch.equal(f1, h1) and torch.equal(f2, h2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nul_line", [None, 0, 1, 99998, 99999])
+def test_device_scan_long_multiline_key(cuda, nul_line):
+    """A key spread over 100000 TAB-less lines before its TAB line (the getline loop keeps
+    appending them), with or without a NUL in one of them: the device scan cuts the key
+    at the first NUL in O(1) through the reverse NUL-line scan, same records as
+    the host scan."""
+    lines = [b"ab%d" % i for i in range(100000)]
+    if nul_line is not None:
+        lines[nul_line] = lines[nul_line][:1] + b"\x00" + lines[nul_line][1:]
+    data = b"x\tfirst\n" + b"\n".join(lines) + b"\tvalue\nlast\tv\n"
+    for shift in (0, 3):
+        _, _, got = _dev_scan_np(cuda, data, "tsv", shift)
+        assert np.array_equal(got, archive.import_scan(data, "tsv")), (nul_line, shift)
