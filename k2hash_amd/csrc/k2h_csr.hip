@@ -328,7 +328,7 @@ enum {
   kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
   kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10,
   kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13, kModeLean2Group = 14,
-  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21
+  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -733,12 +733,13 @@ __device__ __forceinline__ uint64_t second_from_first(uint64_t h1v, uint32_t len
 // key 1 (k1 chunks, 0 = none), end-aligned chunks read from LDS, the switch to key 1
 // (save key 0's state, restart from key 1's S_p with its masked chunk 0) in a branch
 // that only the lanes switching at that step take.  Returns the two h1 values.
+template <bool Z = false>
 __device__ __forceinline__ void pair_walk(uint32_t k0, uint32_t p0, const uint8_t* cp0, uint32_t k1, uint32_t p1,
                                           const uint8_t* cp1, const uint64_t* spad, const uint4* masks,
                                           uint64_t& h0, uint64_t& h1v) {
   const uint32_t T = k0 + k1, sw = k0;
   uint64_t st = spad[p0];
-  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32);
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), z = 0;  // Z: the mad64 zero half kept in v50
   const uint8_t* cp = cp0;
   uint4 m = masks[p0];
   uint4 c0 = ld16(cp0);
@@ -750,7 +751,8 @@ __device__ __forceinline__ void pair_walk(uint32_t k0, uint32_t p0, const uint8_
     uint32_t t = 0;
     for (;;) {
       c1 = ld16(cp + 16u * (t + 1));
-      fnv_chunk16<0>(lo, hi, c0);
+      if constexpr (Z) fnv_chunk16z<0>(lo, hi, c0, z);
+      else fnv_chunk16<0>(lo, hi, c0);
       ++t;
       if (t == sw) {
         saved = pack2(lo, hi);
@@ -767,7 +769,8 @@ __device__ __forceinline__ void pair_walk(uint32_t k0, uint32_t p0, const uint8_
         break;
       }
       c0 = ld16(cp + 16u * (t + 1));
-      fnv_chunk16<1>(lo, hi, c1);
+      if constexpr (Z) fnv_chunk16z<1>(lo, hi, c1, z);
+      else fnv_chunk16<1>(lo, hi, c1);
       ++t;
       if (t == sw) {
         saved = pack2(lo, hi);
@@ -783,7 +786,8 @@ __device__ __forceinline__ void pair_walk(uint32_t k0, uint32_t p0, const uint8_
     }
   }
   if (odd) c0 = c1;
-  fnv_chunk16<0>(lo, hi, c0);  // the last chunk of the lane's last key
+  if constexpr (Z) fnv_chunk16z<0>(lo, hi, c0, z);  // the last chunk of the lane's last key
+  else fnv_chunk16<0>(lo, hi, c0);
   if (k1) {
     h0 = saved;
     h1v = pack2(lo, hi);
@@ -1010,7 +1014,8 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
 //    10.3 us tile life in round 1, profiles/r01f_csr_phases_sortfix.txt).
 // Tiles whose span exceeds the stage are listed for the ring kernel, as in lean2.
 // ---------------------------------------------------------------------------
-template <bool H2, bool EPI, int NW, int STAGE_KIB, bool PERSIST, bool STAGGER = false, bool W2 = false>
+template <bool H2, bool EPI, int NW, int STAGE_KIB, bool PERSIST, bool STAGGER = false, bool W2 = false,
+          bool Z = false>
 __global__ __launch_bounds__(NW * 64) void fnv_csr_pair_kernel(const uint8_t* __restrict__ bytes,
                                                                const uint64_t* __restrict__ offsets, uint64_t n,
                                                                SpadTable spad_tab, uint64_t* __restrict__ h1,
@@ -1158,8 +1163,8 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_pair_kernel(const uint8_t* __
         pair_walk2(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
                    s_spad, s_mask, hw0, hw1);
       else
-        pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
-                  hw0, hw1);
+        pair_walk<Z>(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad,
+                     s_mask, hw0, hw1);
       const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
       if (has_a) {
         h1[t0 + ka] = hA;
@@ -1339,10 +1344,10 @@ static hipError_t launch_lean2(const uint8_t* b, const uint64_t* offsets, uint64
   return hipGetLastError();
 }
 
-// Resident blocks of a kernel per device (occupancy x CUs), computed once per device and
-// kernel; safe to call from any thread.
-template <typename K>
-static unsigned resident_grid(K kernel, int threads, unsigned cap) {
+// Resident blocks of kernel K per device (occupancy x CUs), computed once per device and
+// kernel (the cache is per template instance, i.e. per kernel); safe from any thread.
+template <auto K>
+static unsigned resident_grid(int threads, unsigned cap) {
   constexpr int kMaxDev = 64;
   static std::atomic<unsigned> cache[kMaxDev];
   int dev = 0;
@@ -1350,8 +1355,7 @@ static unsigned resident_grid(K kernel, int threads, unsigned cap) {
   unsigned g = cache[dev].load(std::memory_order_relaxed);
   if (!g) {
     int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kernel, threads, 0) != hipSuccess ||
-        per_cu <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)K, threads, 0) != hipSuccess || per_cu <= 0)
       per_cu = 1;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
     g = (unsigned)(per_cu * cus);
@@ -1361,7 +1365,7 @@ static unsigned resident_grid(K kernel, int threads, unsigned cap) {
 }
 
 // pair-tile kernel (TK = 128 NW keys) + the ring pass over its oversize-tile list
-template <int NW, int KIB, bool PERSIST, bool STAGGER = false, bool W2 = false>
+template <int NW, int KIB, bool PERSIST, bool STAGGER = false, bool W2 = false, bool Z = false>
 static hipError_t launch_pair(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
                               uint64_t* h2, const BucketParams* bp, hipStream_t stream) {
   constexpr uint64_t TK = 128 * NW;
@@ -1376,8 +1380,8 @@ static hipError_t launch_pair(const uint8_t* b, const uint64_t* offsets, uint64_
   const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
 #define K2H_PAIR(H2, EPI)                                                                                        \
   {                                                                                                            \
-    auto k = fnv_csr_pair_kernel<H2, EPI, NW, KIB, PERSIST, STAGGER, W2>;                                                   \
-    const unsigned g = PERSIST ? resident_grid(k, NW * 64, (unsigned)ntiles) : (unsigned)ntiles;               \
+    constexpr auto k = fnv_csr_pair_kernel<H2, EPI, NW, KIB, PERSIST, STAGGER, W2, Z>;                            \
+    const unsigned g = PERSIST ? resident_grid<k>(NW * 64, (unsigned)ntiles) : (unsigned)ntiles;               \
     k<<<g, NW * 64, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, scratch + 1, scratch, p);            \
     fnv_csr_ring_list_kernel<H2, EPI, (int)TK><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, \
                                                                        scratch + 1, scratch, p);               \
@@ -1403,6 +1407,7 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModePair2P) return launch_pair<2, 36, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair4P) return launch_pair<4, 72, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair4) return launch_pair<4, 72, false>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModePair4Z) return launch_pair<4, 72, false, false, false, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair4W2) return launch_pair<4, 72, false, false, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair4PS) return launch_pair<4, 72, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair2PS) return launch_pair<2, 36, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);

@@ -88,6 +88,7 @@ enum {
   kVariantCsrPair4 = 64,          // ... 512 keys, 4 waves, 72 KiB
   kVariantCsrPair4PS = 66,        // csr pair tiles, persistent, second half of the grid starts half a tile late
   kVariantCsrPair2PS = 67,
+  kVariantCsrPair4Z = 69,         // csr pair tiles (512 keys), the mad64 zero half kept in v50 across the walk
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };
