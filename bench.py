@@ -281,14 +281,19 @@ def valu_fields(name: str, kern_s: float, model_insts: float) -> dict:
     """VALU-issue roofline: wave64 VALU instructions per launch (rocprofv3 SQ_INSTS_VALU pass,
     profiles/valu_<name>.json, else the FNV-step model) at the peak issue rate, over the
     measured launch time."""
-    insts, src = model_insts, "model: 86 slow-issue VALU ops per 16-byte chunk per 64 keys"
+    insts, src, clock = model_insts, "model: 86 slow-issue VALU ops per 16-byte chunk per 64 keys", None
     prof = ROOT / "profiles" / f"valu_{name}.json"
     if prof.exists():
         d = json.loads(prof.read_text())
         insts, src = float(d["valu_insts_per_launch"]), f"profiles/valu_{name}.json ({d.get('round', '')})"
+        clock = d.get("clock_ghz")
     floor_s = insts * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_PEAK_HZ)
-    return {"valu_frac": floor_s / kern_s, "valu_insts_per_launch": insts, "valu_floor_us": floor_s * 1e6,
-            "valu_source": src}
+    r = {"valu_frac": floor_s / kern_s, "valu_insts_per_launch": insts, "valu_floor_us": floor_s * 1e6,
+         "valu_source": src}
+    if clock:  # the same floor at the clock the chip holds under this kernel (power-limited)
+        r["valu_frac_at_measured_clock"] = floor_s * VALU_PEAK_HZ / (clock * 1e9) / kern_s
+        r["measured_clock_ghz"] = clock
+    return r
 
 
 def traffic_of(name: str):

@@ -1546,7 +1546,7 @@ static hipError_t launch_fixed_long_lab(const void* keys, uint64_t key_len, uint
     // kLongLines2Pad / Pad2: 4 / 2 KiB of dynamic LDS on top of the 16 KiB ring, i.e. 8 or
     // 9 instead of 10 waves per CU (occupancy probes)
     const unsigned pad = mode == kLongLines2Pad ? 4096u : mode == kLongLines2Pad2 ? 2048u : 0u;
-    if (mode >= kLongProbeCompute) {  // timing probes (wrong hashes)
+    if (mode >= kLongProbeCompute && mode <= kLongProbeMemHalf4) {  // timing probes (wrong hashes)
       if (mode == kLongProbeCompute)
         fnv_fixed_lines_kernel<false, 2, 128, false, 1><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
       else if (mode == kLongProbeMemory)
@@ -1569,6 +1569,7 @@ static hipError_t launch_fixed_long_lab(const void* keys, uint64_t key_len, uint
       case kLongLines3: K2H_LINES(3, 128) break;
       case kLongHalf5: K2H_LINES(5, 64) break;
       case kLongHalf3: K2H_LINES(3, 64) break;
+      case kLongHalf2: K2H_LINES(2, 64) break;
       case kLongHalf4: K2H_LINES(4, 64) break;
       case kLongHalf6: K2H_LINES(6, 64) break;
       default: K2H_LINES(2, 128) break;

@@ -88,6 +88,7 @@ enum {
   kVariantCsrPair4 = 64,          // ... 512 keys, 4 waves, 72 KiB
   kVariantCsrPair4PS = 66,        // csr pair tiles, persistent, second half of the grid starts half a tile late
   kVariantCsrPair2PS = 67,
+  kVariantLongHalf2 = 70,         // fixed long keys: 2 half-line rounds (8 KiB ring per wave)
   kVariantCsrPair4Z = 69,         // csr pair tiles (512 keys), the mad64 zero half kept in v50 across the walk
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
@@ -188,7 +189,8 @@ enum { kLongAuto = 0, kLongDirect = 1, kLongRing = 2, kLongLines2 = 3,
        // timing probes (wrong hashes), keep last: no DMA / DMA only at (D, RB) =
        // (2,128) (2,128) (3,128) (4,128) (2,256) (4,64)
        kLongProbeCompute = 12, kLongProbeMemory = 13, kLongProbeMem3 = 14, kLongProbeMem4 = 15,
-       kLongProbeMem256 = 16, kLongProbeMemHalf4 = 17
+       kLongProbeMem256 = 16, kLongProbeMemHalf4 = 17,
+       kLongHalf2 = 18  // 2 half-line rounds (8 KiB per wave, 20 waves per CU)
 #endif
 };
 bool fixed_lines_ok(const void* keys, uint64_t key_len);

@@ -645,6 +645,7 @@ static hipError_t launch_fixed_lab(const void* keys, uint64_t key_len, uint64_t 
                      : variant == kVariantLongLines2 ? kLongLines2
                      : variant == kVariantLongLines3 ? kLongLines3
                      : variant == kVariantLongHalf3  ? kLongHalf3
+                     : variant == kVariantLongHalf2  ? kLongHalf2
                      : variant == kVariantLongHalf4  ? kLongHalf4
                      : variant == kVariantLongHalf6  ? kLongHalf6
                      : variant == kVariantLongHalf5  ? kLongHalf5

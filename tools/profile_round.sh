@@ -14,7 +14,7 @@ prof() {  # name, args for bench.py
   (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
      -d "$R/$OUT/$name" -o run -- python3 "$R/bench.py" "$@" > "$R/$OUT/$name.log" 2>&1) || { echo "PROF $name failed"; tail -5 "$R/$OUT/$name.log"; exit 1; }
   grep '^{' "$R/$OUT/$name.log" > "$R/$OUT/bench_$name.out" || true
-  local short="--steps 5 --warmup 1 --warm-ms 1 --no-verify"
+  local short="--steps 10 --warmup 2 --no-verify"  # warmed (150 ms): the clock of the timed region
   local i=0
   for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
     i=$((i+1))
