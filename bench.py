@@ -286,11 +286,13 @@ def valu_fields(name: str, kern_s: float, model_insts: float) -> dict:
     if prof.exists():
         d = json.loads(prof.read_text())
         insts, src = float(d["valu_insts_per_launch"]), f"profiles/valu_{name}.json ({d.get('round', '')})"
-        clock = d.get("clock_ghz")
+    probe = ROOT / "profiles" / "clock_probe.json"  # tools/clock_probe.py: s_memtime / s_memrealtime per wave
+    if probe.exists():
+        clock = json.loads(probe.read_text()).get(name, {}).get("clock_ghz")
     floor_s = insts * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_PEAK_HZ)
     r = {"valu_frac": floor_s / kern_s, "valu_insts_per_launch": insts, "valu_floor_us": floor_s * 1e6,
          "valu_source": src}
-    if clock:  # the same floor at the clock the chip holds under this kernel (power-limited)
+    if clock:  # the same floor at the shader clock the waves ran at under this kernel (power-limited)
         r["valu_frac_at_measured_clock"] = floor_s * VALU_PEAK_HZ / (clock * 1e9) / kern_s
         r["measured_clock_ghz"] = clock
     return r

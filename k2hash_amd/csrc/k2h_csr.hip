@@ -1272,6 +1272,11 @@ __global__ __launch_bounds__(64) void fnv_fixed_lines_kernel(const uint8_t* __re
                                        (__attribute__((address_space(3))) void*)(slot + 1024u * i), 16, 0, 0);
   };
 
+  uint64_t clk0 = 0, rt0 = 0;
+  if constexpr (PROBE == 3) {  // clock probe: h2 receives per wave the shader-clock / 100 MHz stamps
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   for (uint32_t q = 0; q < D - 1 && q < R; ++q) issue(q);
   uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2 = lo, hi2 = hi;
   for (uint32_t q = 0; q < R; ++q) {
@@ -1297,11 +1302,21 @@ __global__ __launch_bounds__(64) void fnv_fixed_lines_kernel(const uint8_t* __re
       fnv_lds_round_last<NP>(lo, hi, lo2, hi2, a);  // the state before the key's final byte
     }
   }
+  if constexpr (PROBE == 3) {
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    if (t == 0) {
+      uint64_t* o = h2 + 4ull * blockIdx.x;
+      o[0] = clk0;
+      o[1] = clk1;
+      o[2] = rt0;
+      o[3] = rt1;
+    }
+  }
   if (t > last) return;
   const uint64_t i = key0 + t;
   const uint64_t r1 = pack2(lo, hi);
   __builtin_nontemporal_store(r1, h1 + i);
-  if constexpr (H2) __builtin_nontemporal_store(pack2(lo2, hi2), h2 + i);
+  if constexpr (H2 && PROBE != 3) __builtin_nontemporal_store(pack2(lo2, hi2), h2 + i);
   if constexpr (EPI) bucket_emit(bp, i, r1);
 }
 
@@ -1546,7 +1561,7 @@ static hipError_t launch_fixed_long_lab(const void* keys, uint64_t key_len, uint
     // kLongLines2Pad / Pad2: 4 / 2 KiB of dynamic LDS on top of the 16 KiB ring, i.e. 8 or
     // 9 instead of 10 waves per CU (occupancy probes)
     const unsigned pad = mode == kLongLines2Pad ? 4096u : mode == kLongLines2Pad2 ? 2048u : 0u;
-    if (mode >= kLongProbeCompute && mode <= kLongProbeMemHalf4) {  // timing probes (wrong hashes)
+    if ((mode >= kLongProbeCompute && mode <= kLongProbeMemHalf4) || mode == kLongProbeClock) {  // probes
       if (mode == kLongProbeCompute)
         fnv_fixed_lines_kernel<false, 2, 128, false, 1><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
       else if (mode == kLongProbeMemory)
@@ -1559,6 +1574,8 @@ static hipError_t launch_fixed_long_lab(const void* keys, uint64_t key_len, uint
         fnv_fixed_lines_kernel<false, 2, 256, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
       else if (mode == kLongProbeMemHalf4)
         fnv_fixed_lines_kernel<false, 4, 64, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      else if (mode == kLongProbeClock && h2)
+        fnv_fixed_lines_kernel<true, 2, 128, false, 3><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, h2);
       return hipGetLastError();
     }
     if (mode == kLongLines256 && key_len % 256 != 0) mode = kLongLines2;

@@ -89,6 +89,13 @@ enum {
   kVariantCsrPair4PS = 66,        // csr pair tiles, persistent, second half of the grid starts half a tile late
   kVariantCsrPair2PS = 67,
   kVariantLongHalf2 = 70,         // fixed long keys: 2 half-line rounds (8 KiB ring per wave)
+  kVariantFixed32Clock = 71,      // clock probes: the default fixed32 / 4 KiB kernels, h2 = per-wave stamps of the
+  kVariantLongClock = 72,         // shader clock (s_memtime) and the 100 MHz counter (tools/clock_probe.py)
+  kVariantRalleGroup8 = 73,       // ralledata: the round-1/2 group kernel (8 lanes per record, unaligned stores)
+  kVariantRalleGather = 74,       // ralledata: output-driven gather from LDS-staged segments (aligned line stores)
+  kVariantRalleGatherFused = 75,  // ... with the key hashes computed in the same kernel from the staged keys (default)
+  kVariantRallePhases = 76,       // the one-shot gather form with per-block phase stamps in blob_off (tools/ralle_phases.py)
+  kVariantRallePhasesNoStore = 77,  // ... and no piece stores (timing probe, wrong blobs)
   kVariantCsrPair4Z = 69,         // csr pair tiles (512 keys), the mad64 zero half kept in v50 across the walk
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
@@ -190,7 +197,8 @@ enum { kLongAuto = 0, kLongDirect = 1, kLongRing = 2, kLongLines2 = 3,
        // (2,128) (2,128) (3,128) (4,128) (2,256) (4,64)
        kLongProbeCompute = 12, kLongProbeMemory = 13, kLongProbeMem3 = 14, kLongProbeMem4 = 15,
        kLongProbeMem256 = 16, kLongProbeMemHalf4 = 17,
-       kLongHalf2 = 18  // 2 half-line rounds (8 KiB per wave, 20 waves per CU)
+       kLongHalf2 = 18,  // 2 half-line rounds (8 KiB per wave, 20 waves per CU)
+       kLongProbeClock = 19  // clock probe (h2 = per-wave shader-clock / 100 MHz stamps)
 #endif
 };
 bool fixed_lines_ok(const void* keys, uint64_t key_len);

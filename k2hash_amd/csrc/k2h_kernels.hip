@@ -254,10 +254,17 @@ __global__ __launch_bounds__(256) void fnv_fixed32_lds_kernel(const uint4* __res
 // fixed32, flat grid, KPT keys per thread: block b owns keys [b*256*KPT, (b+1)*256*KPT);
 // thread t hashes keys b*256*KPT + j*256 + t.  All 2*KPT loads are issued before the
 // first hash, so each wave keeps KPT*2 KiB in flight while it computes.
-template <bool H2, int KPT, int BS = 256, bool NT = false, bool EPI = false>
+template <bool H2, int KPT, int BS = 256, bool NT = false, bool EPI = false, bool CLK = false>
 __global__ __launch_bounds__(BS) void fnv_fixed32_kpt_kernel(const uint4* __restrict__ keys, uint64_t n,
                                                              uint64_t seed, uint64_t* __restrict__ h1,
                                                              uint64_t* __restrict__ h2, BucketParams bp = {}) {
+  // CLK (lab clock probe, h1 only): h2 receives per wave the shader-clock and 100 MHz
+  // counters at its start and end (tools/clock_probe.py)
+  uint64_t clk0 = 0, rt0 = 0;
+  if constexpr (CLK) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   const uint64_t base = (uint64_t)blockIdx.x * (BS * KPT) + threadIdx.x;
   uint4 a[KPT], b[KPT];
 #pragma unroll
@@ -290,6 +297,16 @@ __global__ __launch_bounds__(BS) void fnv_fixed32_kpt_kernel(const uint4* __rest
       } else {
         fixed32_hash_store(a[j], b[j], seed, i, h1, h2, H2);
       }
+    }
+  }
+  if constexpr (CLK) {
+    const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63u) == 0) {
+      uint64_t* o = h2 + 4ull * (blockIdx.x * (BS / 64) + threadIdx.x / 64);
+      o[0] = clk0;
+      o[1] = clk1;
+      o[2] = rt0;
+      o[3] = rt1;
     }
   }
 }
@@ -588,6 +605,12 @@ static hipError_t launch_fixed_lab(const void* keys, uint64_t key_len, uint64_t 
         if (h2) fnv_fixed32_x_kernel<true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_x_kernel<false><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
+      case kVariantFixed32Clock: {  // clock probe: h2 = stamps (4 per wave), h1 hashes
+        if (!h2) return hipErrorInvalidValue;
+        unsigned g = (unsigned)((n + 127) / 128);
+        fnv_fixed32_kpt_kernel<false, 2, 64, true, false, true><<<g, 64, 0, stream>>>(k, n, seed, h1, h2);
+        break;
+      }
       case kVariantFixed32Flat:
         if (h2) fnv_fixed32_kernel<true, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, h2);
         else fnv_fixed32_kernel<false, true><<<grid_for(n), 256, 0, stream>>>(k, n, seed, h1, nullptr);
@@ -646,6 +669,7 @@ static hipError_t launch_fixed_lab(const void* keys, uint64_t key_len, uint64_t 
                      : variant == kVariantLongLines3 ? kLongLines3
                      : variant == kVariantLongHalf3  ? kLongHalf3
                      : variant == kVariantLongHalf2  ? kLongHalf2
+                     : variant == kVariantLongClock  ? kLongProbeClock
                      : variant == kVariantLongHalf4  ? kLongHalf4
                      : variant == kVariantLongHalf6  ? kLongHalf6
                      : variant == kVariantLongHalf5  ? kLongHalf5

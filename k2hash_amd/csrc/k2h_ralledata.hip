@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "k2h_fnv_device.h"
 #include "k2h_kernels.h"
 
 namespace k2h {
@@ -130,6 +131,310 @@ __global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, ui
   if (blob_off && q == 0) {
     blob_off[i] = o;
     if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
+  }
+}
+
+// Gather form (round 2): output-driven.  A block takes R consecutive records; its blobs are
+// one contiguous output span, and the records' key / value / subkey / attribute bytes are
+// four contiguous input spans.  The block
+//   1. stages the four input spans into LDS with aligned 16-byte loads (the aligned hull of
+//      each span: every load holds a valid byte, so none leaves a mapped page) and builds
+//      the R headers in LDS, plus a table of the span's segments (header, key, value,
+//      subkeys, attrs of each record: where each starts in the span and where its bytes sit
+//      in LDS) and, per aligned 16-byte output piece, the segment holding its first byte;
+//   2. writes the span as aligned 16-byte pieces, consecutive lanes on consecutive pieces
+//      (whole 128-byte lines per 8 lanes): a piece is one unaligned ds_read_b128 from the
+//      segment that holds it, or, where segments meet inside it, one read per segment
+//      merged under a byte mask.  Only the two pieces a block shares with its neighbours
+//      are stored byte by byte.
+// So every blob byte is stored once, aligned, and every input byte is loaded once, aligned;
+// the group form's unaligned 16-byte accesses at ~2.3 TB/s are gone.  A block whose spans
+// exceed the LDS image (records much larger than BASELINE-like ones) runs the group form.
+constexpr int kGatherRecs = 64;                  // records per 256-thread block
+constexpr int kGatherPool = 12288;               // staged segment bytes (BASELINE-like: ~10.5 KB, sd ~0.6 KB; 7 blocks per CU)
+constexpr int kGatherHdr = 16;                   // LDS offset of the headers (16 readable bytes below)
+constexpr int kGatherImg = kGatherHdr + 80 * kGatherRecs + kGatherPool + 16;
+constexpr int kGatherPieces = (80 * kGatherRecs + kGatherPool) / 16 + 2;
+
+// Key hash straight from HBM (the fused kernel's group-form blocks): the same end-aligned
+// chunks; bytes below the key buffer are never read.
+__device__ __forceinline__ void global_key_hash(const uint8_t* keys, uint64_t b, uint64_t e, const uint64_t* spad,
+                                                uint64_t& r1, uint64_t& r2) {
+  const uint64_t len = e - b, k = (len + 15) >> 4;
+  const uint32_t p = (uint32_t)(16 * k - len);
+  const uint8_t* cp = keys + e - 16 * k;
+  const uint64_t st = spad[p & 15];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2 = lo, hi2 = hi;
+  uint32_t w[4] = {0, 0, 0, 0};
+  for (uint32_t j = p; j < 16 && k; ++j) w[j >> 2] |= (uint32_t)cp[j] << (8 * (j & 3));
+  uint4 c = make_uint4(w[0], w[1], w[2], w[3]);
+  for (uint64_t j = 1; j < k; ++j) {
+    fnv_chunk16(lo, hi, c);
+    const u32x4_ua v = *reinterpret_cast<const u32x4_ua*>(cp + 16 * j);
+    c = make_uint4(v.x, v.y, v.z, v.w);
+  }
+  fnv_chunk16_last(lo, hi, lo2, hi2, c);
+  r1 = k ? ((uint64_t)hi << 32) | lo : 0;
+  r2 = k ? (len == 1 ? r1 : ((uint64_t)hi2 << 32) | lo2) : 0;
+}
+
+// one record by a group of G lanes, straight to HBM (the group form); HASH: lane 0 hashes
+// the key itself instead of reading h
+template <int G, bool HASH = false>
+__device__ __forceinline__ void group_record(const RalleInputs& in, uint64_t n, const uint64_t* __restrict__ h,
+                                             uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off,
+                                             uint64_t i, uint32_t q, const uint64_t* spad = nullptr) {
+  const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i), al = seg_len(in.aoff, i);
+  const uint64_t o = 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) +
+                     seg_before(in.aoff, i);
+  uint8_t* b = out + o;
+  if (q < 5) {
+    uint64_t f0, f1;
+    switch (q) {
+      case 0:
+        if constexpr (HASH) {
+          if (in.koff) global_key_hash(in.keys, in.koff[i], in.koff[i + 1], spad, f0, f1);
+          else f0 = f1 = 0;
+        } else {
+          f0 = h[i];
+          f1 = h[n + i];
+        }
+        break;
+      case 1: f0 = kl; f1 = vl; break;
+      case 2: f0 = sl; f1 = al; break;
+      case 3: f0 = 80; f1 = 80 + kl; break;
+      default: f0 = 80 + kl + vl; f1 = 80 + kl + vl + sl; break;
+    }
+    *reinterpret_cast<u32x4_ua*>(b + 16 * q) = u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
+  }
+  if (kl) group_copy<G>(b + 80, in.keys + in.koff[i], kl, q);
+  if (vl) group_copy<G>(b + 80 + kl, in.vals + in.voff[i], vl, q);
+  if (sl) group_copy<G>(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
+  if (al) group_copy<G>(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
+  if (blob_off && q == 0) {
+    blob_off[i] = o;
+    if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
+  }
+}
+
+// Key hash from the staged bytes (FUSED): end-aligned 16-byte chunks (the CSR kernels'
+// scheme): chunk 0 starts 16k - len bytes early with those bytes
+// zeroed and the state started at S_p = seed * P^-p, so no byte tail; the last chunk's
+// byte 15 step leaves the second hash (the state before the last byte).
+__device__ __forceinline__ void staged_key_hash(const uint8_t* end, uint32_t len, const uint64_t* spad, uint64_t& r1,
+                                                uint64_t& r2) {
+  const uint32_t k = (len + 15) >> 4, p = 16 * k - len;
+  const uint8_t* cp = end - 16 * k;
+  const uint64_t st = spad[p & 15];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32), lo2 = lo, hi2 = hi;
+  u32x4_ua w = *reinterpret_cast<const u32x4_ua*>(cp);
+  const int32_t sh = (int32_t)(8 * p);
+  auto lead = [sh](int32_t b) -> uint32_t { return (uint32_t)(~0ull << min(max(sh - b, 0), 32)); };
+  uint4 c = make_uint4(w.x & lead(0), w.y & lead(32), w.z & lead(64), w.w & lead(96));
+  for (uint32_t j = 1; j < k; ++j) {
+    fnv_chunk16(lo, hi, c);
+    w = *reinterpret_cast<const u32x4_ua*>(cp + 16 * j);
+    c = make_uint4(w.x, w.y, w.z, w.w);
+  }
+  fnv_chunk16_last(lo, hi, lo2, hi2, c);
+  r1 = k ? ((uint64_t)hi << 32) | lo : 0;  // empty key hashes to 0 (lib/k2hashfunc.cc:66-68, 80-82)
+  r2 = k ? (len == 1 ? r1 : ((uint64_t)hi2 << 32) | lo2) : 0;
+}
+
+// FUSED: the key hashes are computed here from the staged key bytes (no hash kernel, no
+// scratch); otherwise h holds h1[n] then h2[n] from the CSR hash kernel.  PROBE (lab,
+// tools/ralle_phases.py): thread 0 overwrites blob_off[r0 .. r0+4] with shader-clock
+// stamps at entry, after each barrier and at the end of its pieces (wrong offsets).
+template <bool FUSED, int PROBE = 0>  // PROBE 1: stamps, 2: stamps + no piece stores (timing only)
+__global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
+                                                               uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off,
+                                                               SpadTable spad_tab) {
+  constexpr int R = kGatherRecs, NSEG = 5 * R;
+  typedef uint32_t u32x4_al __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) uint8_t img[kGatherImg];
+  __shared__ int2 seg[NSEG + 1];     // segment g: .x = adj (span byte y sits at img[y + adj]), .y = its end in the span
+  __shared__ uint16_t tab[kGatherPieces];  // segment holding piece p's first byte
+  __shared__ u32x4_al qmask[17];
+  __shared__ uint64_t spad[16];
+  const uint32_t tid = threadIdx.x;
+  uint64_t t0 = 0, t1 = 0, t2 = 0;
+  if constexpr (PROBE) t0 = __builtin_amdgcn_s_memtime();
+  const uint64_t r0 = (uint64_t)blockIdx.x * R;
+  const uint32_t nr = (uint32_t)(n - r0 < (uint64_t)R ? n - r0 : (uint64_t)R);
+  const uint64_t* offs[4] = {in.koff, in.voff, in.soff, in.aoff};
+  const uint8_t* srcs[4] = {in.keys, in.vals, in.skeys, in.attrs};
+  // block-uniform: each input span, its aligned hull, where it goes in the image
+  uint64_t o_first = 80ull * r0, span = 80ull * nr, hull_total = 0;
+  uint64_t sbase[4], hull_lo[4], hull_n[4];
+  int32_t area[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint64_t b = 0, e = 0, f = 0;
+    if (offs[s]) {
+      b = offs[s][r0];
+      e = offs[s][r0 + nr];
+      f = offs[s][0];
+    }
+    sbase[s] = b;
+    o_first += b - f;
+    span += e - b;
+    const uint64_t lo = (uint64_t)(uintptr_t)(srcs[s] + b) & ~15ull, hi = ((uint64_t)(uintptr_t)(srcs[s] + e) + 15) & ~15ull;
+    hull_lo[s] = lo;
+    hull_n[s] = e > b ? (hi - lo) >> 4 : 0;
+    area[s] = kGatherHdr + 80 * R + (int32_t)(16 * hull_total) + (int32_t)((uintptr_t)(srcs[s] + b) - lo);
+    hull_total += hull_n[s];
+  }
+  if (16 * hull_total > (uint64_t)kGatherPool) {  // block-uniform: too large to stage
+    if constexpr (FUSED) {
+      // hash then assemble: the group form reads the hashes back from this block's records
+      // (one lane per record, straight from HBM, written to the blobs' first 16 bytes below)
+      if (tid < 16) spad[tid] = spad_tab.v[tid];
+      __syncthreads();
+      for (uint32_t rec = tid / 8; rec < nr; rec += 32) group_record<8, true>(in, n, nullptr, out, blob_off, r0 + rec, tid % 8, spad);
+    } else {
+      for (uint32_t rec = tid / 8; rec < nr; rec += 32) group_record<8>(in, n, h, out, blob_off, r0 + rec, tid % 8);
+    }
+    return;
+  }
+  // 1a. the staged pieces: up to 4 aligned loads per thread, issued first
+  constexpr int PPT = (kGatherPool / 16 + 255) / 256;
+  u32x4_al v[PPT];
+  uint32_t dst[PPT];
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    uint64_t q = tid + 256u * u;
+    dst[u] = 0xffffffffu;
+    if (q < hull_total) {
+      uint64_t addr = 0, before = 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (q >= before && q < before + hull_n[s]) addr = hull_lo[s] + 16 * (q - before);
+        before += hull_n[s];
+      }
+      v[u] = *reinterpret_cast<const u32x4_al*>((uintptr_t)addr);
+      dst[u] = kGatherHdr + 80 * R + 16 * (uint32_t)q;
+    }
+  }
+  // 1b. one thread per record: header, segment table, piece table, blob offset.  All
+  // block-relative quantities fit 32 bits once the spans fit the image.
+  const uint64_t a_out = (uint64_t)(uintptr_t)(out + o_first);
+  const int32_t d0 = (int32_t)(a_out & 15u);
+  if (tid < 17) {  // qmask[l] = bytes [l, 16) of a piece
+    u32x4_al m;
+    m.x = (uint32_t)(~0ull << (8 * min(max((int)tid - 0, 0), 4)));
+    m.y = (uint32_t)(~0ull << (8 * min(max((int)tid - 4, 0), 4)));
+    m.z = (uint32_t)(~0ull << (8 * min(max((int)tid - 8, 0), 4)));
+    m.w = (uint32_t)(~0ull << (8 * min(max((int)tid - 12, 0), 4)));
+    qmask[tid] = m;
+  }
+  if (FUSED && tid < 16) spad[tid] = spad_tab.v[tid];
+  if (tid < nr) {
+    const uint64_t i = r0 + tid;
+    uint32_t rel[4], len[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint32_t o0 = offs[s] ? (uint32_t)offs[s][i] : 0u, o1 = offs[s] ? (uint32_t)offs[s][i + 1] : 0u;
+      rel[s] = o0 - (uint32_t)sbase[s];
+      len[s] = o1 - o0;
+    }
+    const int32_t B = (int32_t)(80u * tid + rel[0] + rel[1] + rel[2] + rel[3]);
+    const uint32_t kl = len[0], vl = len[1], sl = len[2], al = len[3];
+    uint64_t h1 = 0, h2 = 0;
+    if constexpr (!FUSED) {
+      h1 = h[i];
+      h2 = h[n + i];
+    }
+    const uint32_t f[20] = {(uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32), kl, 0, vl, 0, sl, 0,
+                            al, 0, 80, 0, 80 + kl, 0, 80 + kl + vl, 0, 80 + kl + vl + sl, 0};
+#pragma unroll
+    for (int c = 0; c < 5; ++c)
+      *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid + 16 * c) = u32x4_al{f[4 * c], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]};
+    int32_t start = B;
+    int32_t p = tid == 0 ? 0 : (B + d0 + 15) >> 4;  // first piece whose first byte is in this record
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      const uint32_t g = 5 * tid + c;
+      const int32_t L = c == 0 ? 80 : (int32_t)len[c - 1];
+      const int32_t adj = c == 0 ? kGatherHdr + 80 * (int32_t)tid - start : area[c - 1] + (int32_t)rel[c - 1] - start;
+      seg[g] = int2{adj, start + L};
+      for (; 16 * p - d0 < start + L; ++p) tab[p] = (uint16_t)g;  // pieces starting in this segment
+      start += L;
+    }
+    if (tid + 1 == nr) seg[5 * nr] = int2{kGatherHdr, start};  // read (never used) as the last segment's successor
+    if (blob_off) {
+      blob_off[i] = o_first + B;
+      if (i + 1 == n) blob_off[n] = o_first + start;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PPT; ++u)
+    if (dst[u] != 0xffffffffu) *reinterpret_cast<u32x4_al*>(img + dst[u]) = v[u];
+  __syncthreads();
+  if constexpr (PROBE) t1 = __builtin_amdgcn_s_memtime();
+  if constexpr (FUSED) {  // 1c. wave 0 hashes the block's keys from the image into the headers
+    if (tid < nr) {
+      const uint32_t kl = in.koff ? (uint32_t)in.koff[r0 + tid + 1] - (uint32_t)in.koff[r0 + tid] : 0u;
+      const uint32_t ke = in.koff ? (uint32_t)in.koff[r0 + tid + 1] - (uint32_t)sbase[0] : 0u;
+      uint64_t h1, h2;
+      staged_key_hash(img + area[0] + ke, kl, spad, h1, h2);
+      *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid) =
+          u32x4_al{(uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32)};
+    }
+    __syncthreads();
+  }
+  if constexpr (PROBE) t2 = __builtin_amdgcn_s_memtime();
+  // 2. aligned output pieces: the window of each segment in the piece, aligned with the
+  // piece, merged forward (segment k supplies bytes [its start, 16) over what came before)
+  const int32_t sp = (int32_t)span;
+  const uint32_t np = (uint32_t)((d0 + sp + 15) >> 4);
+  uint8_t* const base = out + (o_first - (uint64_t)d0);
+  for (uint32_t p = tid; p < np; p += 256) {
+    const int32_t x = 16 * (int32_t)p - d0, end = min(x + 16, sp);
+    uint32_t g = tab[p];
+    // the piece's segment and the next one in one read, both windows read together
+    const int2 s0 = seg[g], s1 = seg[g + 1];
+    const u32x4_ua w0 = *reinterpret_cast<const u32x4_ua*>(img + s0.x + x);
+    const u32x4_ua w1 = *reinterpret_cast<const u32x4_ua*>(img + s1.x + x);
+    u32x4_al acc = {w0.x, w0.y, w0.z, w0.w};
+    int32_t pos = s0.y;
+    auto merge = [&](const u32x4_ua& w) {  // bytes [pos - x, 16) from w
+      const u32x4_al q = qmask[pos - x];
+      acc.x = (w.x & q.x) | (acc.x & ~q.x);
+      acc.y = (w.y & q.y) | (acc.y & ~q.y);
+      acc.z = (w.z & q.z) | (acc.z & ~q.z);
+      acc.w = (w.w & q.w) | (acc.w & ~q.w);
+    };
+    if (pos < end) {
+      if (s1.y > pos) {
+        merge(w1);
+        pos = s1.y;
+      }
+      ++g;
+      while (pos < end) {  // a third segment starts in this piece (a short or empty one between)
+        const int2 sn = seg[++g];
+        if (sn.y > pos) {
+          merge(*reinterpret_cast<const u32x4_ua*>(img + sn.x + x));
+          pos = sn.y;
+        }
+      }
+    }
+    if (PROBE == 2) {
+      if (acc.x == 0x9e3779b9u && acc.y == p) base[0] = 0;  // keep the gather, drop the stores
+    } else if (x >= 0 && x + 16 <= sp) {
+      __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_al*>(base + 16ull * p));
+    } else {  // shared with a neighbouring block: this block's bytes only
+      const uint32_t wv[4] = {acc.x, acc.y, acc.z, acc.w};
+      for (int k = max(0, -x); k < 16 && x + k < sp; ++k) base[16ull * p + k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+  if constexpr (PROBE != 0) {
+    const uint64_t t3 = __builtin_amdgcn_s_memtime();
+    if (tid == 0 && nr >= 4) {
+      blob_off[r0] = t0;
+      blob_off[r0 + 1] = t1;
+      blob_off[r0 + 2] = t2;
+      blob_off[r0 + 3] = t3;
+    }
   }
 }
 
@@ -347,12 +652,39 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
     if (blob_off) return hipMemsetAsync(blob_off, 0, 8, stream);
     return hipSuccess;
   }
+#if K2H_AMD_LAB
+  const bool two_kernels = variant == kVariantRalleThread || variant == kVariantRalleProbeAligned ||
+                           variant == kVariantRalleProbeHeader || variant == kVariantRalleGroup16 ||
+                           variant == kVariantRalleByteTail || variant == kVariantRalleBatch4 ||
+                           variant == kVariantRalleBatch2 || variant == kVariantRalleStage ||
+                           variant == kVariantRalleGroup8 || variant == kVariantRalleGather;
+#else
+  constexpr bool two_kernels = false;
+#endif
+#if K2H_AMD_LAB
+  if (variant == kVariantRallePhasesNoStore) {
+    ralledata_gather_kernel<true, 2>
+        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+    return hipGetLastError();
+  }
+  if (variant == kVariantRallePhases) {
+    ralledata_gather_kernel<true, 1>
+        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+    return hipGetLastError();
+  }
+#endif
+  if (!two_kernels) {  // the product: one kernel, hashes computed from the staged keys
+    ralledata_gather_kernel<true>
+        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+    return hipGetLastError();
+  }
+#if K2H_AMD_LAB
+  // lab: the CSR hash kernel writes h1/h2 to stream-ordered scratch, then an assembly kernel
   uint64_t* h = nullptr;
   hipError_t e = hipMallocAsync((void**)&h, 16 * n, stream);
   if (e != hipSuccess) return e;
   e = launch_csr(in.keys, in.koff, n, seed, h, h + n, variant, stream);
   if (e == hipSuccess) {
-#if K2H_AMD_LAB
     if (variant == kVariantRalleThread)
       ralledata_assemble_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
     else if (variant == kVariantRalleProbeAligned)
@@ -370,13 +702,15 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
     else if (variant == kVariantRalleStage)
       ralledata_stage_kernel<kRalleRecsPerBlock, kRalleImage>
           <<<(unsigned)((n + kRalleRecsPerBlock - 1) / kRalleRecsPerBlock), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else
-#endif
+    else if (variant == kVariantRalleGroup8)
       ralledata_group_kernel<8><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
+    else
+      ralledata_gather_kernel<false><<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, h, out, blob_off, SpadTable{});
     e = hipGetLastError();
   }
   hipError_t f = hipFreeAsync(h, stream);
   return e != hipSuccess ? e : f;
+#endif
 }
 
 }  // namespace k2h

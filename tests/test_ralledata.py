@@ -130,3 +130,67 @@ def test_device_nonzero_first_offsets(cuda, oracle):
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), ref)
     assert np.array_equal(boff.cpu().numpy().view(np.uint64), rboff)
+
+
+def _random_records(oracle, n, segments, klen, vlen, slen=(0, 16), alen=(0, 24), big_every=0, seed=0):
+    rng = np.random.default_rng(seed)
+    data = oracle.gen_bytes(n * (klen[1] + vlen[1] + slen[1] + alen[1]) + 64 * 1024 + 16, byte_off=77)
+    pos = 0
+
+    def take(lo, hi, p_empty, big=0):
+        nonlocal pos
+        out = []
+        for i in range(n):
+            L = 0 if rng.random() < p_empty else int(rng.integers(lo, hi))
+            if big and i % big == big - 1:
+                L = 5000
+            out.append(data[pos % (len(data) - 6000):][:L].tobytes())
+            pos += L
+        return out
+    k = take(*klen, 0.02)
+    v = take(*vlen, 0.2, big_every) if "v" in segments else None
+    s = take(*slen, 0.5) if "s" in segments else None
+    a = take(*alen, 0.5) if "a" in segments else None
+    return k, v, s, a
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("segments", ["kv", "k", "kvsa", "ka", "kv_big", "kv_unaligned"])
+def test_device_gather_form_vs_oracle(cuda, oracle, segments):
+    """BASELINE-like records (keys 0-64 B, values 0-200 B): blocks of 64 records are staged
+    in LDS and written as aligned pieces (the gather form); `_big` puts a 5000-B value in
+    every 97th record so some blocks take the group form next to staged ones;
+    `_unaligned` offsets every input and the output by a few bytes."""
+    import torch
+    n = 20011
+    k, v, s, a = _random_records(oracle, n, segments.split("_")[0], (0, 65), (0, 201),
+                                 big_every=97 if segments.endswith("big") else 0, seed=len(segments))
+    ref, rboff = oracle.build_ralledata(k, v, s, a)
+    segs = []
+    shift = 0
+    for x in (k, v, s, a):
+        if x is None:
+            segs += [None, None]
+            continue
+        d, o = _dev(torch, cuda, x)
+        if segments.endswith("unaligned"):
+            shift += 3
+            pad = torch.zeros(d.numel() + shift, dtype=torch.uint8, device=cuda)
+            pad[shift:] = d
+            d, o = pad, o + shift  # same bytes, data pointer still the tensor start: offsets move
+            d = d[1:]
+            o = o - 1
+        segs += [d, o]
+    if segments.endswith("unaligned"):
+        total = len(ref)
+        big = torch.zeros(total + 16, dtype=torch.uint8, device=cuda)
+        out, boff = ralledata.build_ralledata(*segs, out=big[5:5 + total], total=total)
+    else:
+        out, boff = ralledata.build_ralledata(*segs)
+    torch.cuda.synchronize()
+    got = out.cpu().numpy()
+    assert np.array_equal(got, ref), f"first diff at {int(np.argmax(got != ref))}"
+    assert np.array_equal(boff.cpu().numpy().view(np.uint64), rboff)
+    if segments.endswith("unaligned"):
+        b = big.cpu().numpy()
+        assert not b[:5].any() and not b[5 + total:].any()  # nothing outside the blob span

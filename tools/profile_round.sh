@@ -16,9 +16,9 @@ prof() {  # name, args for bench.py
   grep '^{' "$R/$OUT/$name.log" > "$R/$OUT/bench_$name.out" || true
   local short="--steps 10 --warmup 2 --no-verify"  # warmed (150 ms): the clock of the timed region
   local i=0
-  for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE"; do
+  for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES"; do
     i=$((i+1))
-    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex fnv_ \
+    (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex "fnv_|ralledata" \
        --output-format csv -d "$R/$OUT/${name}_pmc$i" -o pmc -- python3 "$R/bench.py" "$@" $short > "$R/$OUT/${name}_pmc$i.log" 2>&1) \
        || { echo "PMC $name pass $i ($c) failed"; tail -5 "$R/$OUT/${name}_pmc$i.log"; exit 1; }
   done

@@ -29,7 +29,8 @@ for d in sorted(p for p in src.iterdir() if p.is_dir() and "_pmc" not in p.name)
     line = json.loads(bench.read_text().strip().splitlines()[-1]) if bench.exists() and bench.read_text().strip() else None
     if not stats or not trace:
         continue
-    rows = [r for r in csv.DictReader(open(stats[0])) if "synth" not in r["Name"] and "fnv_" in r["Name"]]
+    want = "ralledata" if cfg == "ralledata" else "fnv_"  # the config's dominant product kernel
+    rows = [r for r in csv.DictReader(open(stats[0])) if "synth" not in r["Name"] and want in r["Name"]]
     top = max(rows, key=lambda r: float(r["TotalDurationNs"]))
     (dst / f"{tag}_{cfg}_kernel_stats.csv").write_text(open(stats[0]).read())
     disp = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(trace[0]))
@@ -42,23 +43,17 @@ for d in sorted(p for p in src.iterdir() if p.is_dir() and "_pmc" not in p.name)
               "window_span_ns_first_start_to_last_end": win[-1][1] - win[0][0],
               "all_dispatches_avg_ns": float(top["AverageNs"])}
     pmc = {}
-    clocks = []
     for f in glob.glob(str(src / f"{cfg}_pmc*" / "**" / "*counter_collection.csv"), recursive=True):
         per = {}  # dispatch -> counter -> sum over XCDs / SEs
         for r in csv.DictReader(open(f)):
             if r["Kernel_Name"].split("(")[0] == top["Name"].split("(")[0]:
                 d = per.setdefault(r["Dispatch_Id"], {})
                 d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        tr = glob.glob(str(Path(f).parent / "*kernel_trace.csv"))
-        durs = {r["Dispatch_Id"]: int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in csv.DictReader(open(tr[0]))} if tr else {}
         last = sorted(per, key=int)[-10:]  # the timed dispatches of the (warmed) PMC run
         for d in last:
             for c, v in per[d].items():
                 pmc.setdefault(c, []).append(v)
-            if "GRBM_GUI_ACTIVE" in per[d] and durs.get(d):
-                clocks.append(per[d]["GRBM_GUI_ACTIVE"] / 8 / durs[d])  # 8 XCDs; cycles per ns = GHz
     pmc = {k: sum(v) / len(v) for k, v in pmc.items()}
-    clock = sum(clocks) / len(clocks) if clocks else None
     traffic = None
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         traffic = int(2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024)
@@ -70,17 +65,16 @@ for d in sorted(p for p in src.iterdir() if p.is_dir() and "_pmc" not in p.name)
         (dst / f"valu_{cfg}.json").write_text(json.dumps({
             "kernel": top["Name"], "valu_insts_per_launch": pmc["SQ_INSTS_VALU"],
             "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"), "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"),
-            "waves_per_launch": pmc.get("SQ_WAVES"), "clock_ghz": clock,
-            "clock_note": "GRBM_GUI_ACTIVE per XCD / dispatch duration over the PMC run's last 10 dispatches",
+            "waves_per_launch": pmc.get("SQ_WAVES"),
             "source": f"profiles/{tag}_{cfg}_summary.json (rocprofv3 --pmc SQ_INSTS_VALU pass)", "round": tag},
             indent=1))
-    s = {"window": window, "pmc_per_launch": pmc, "hbm_bytes_per_launch": traffic, "clock_ghz": clock}
+    s = {"window": window, "pmc_per_launch": pmc, "hbm_bytes_per_launch": traffic}
     if line:
         kern_ms = line["kernel_ms"]
         s["bench"] = {k: line.get(k) for k in ("value", "ms_per_step", "kernel_ms", "roofline")}
         s["window_vs_bench_event_time"] = window["window_avg_ns"] / 1e6 / kern_ms
     (dst / f"{tag}_{cfg}_summary.json").write_text(json.dumps(s, indent=1))
     summary[cfg] = {"window_avg_us": window["window_avg_ns"] / 1e3, "traffic": traffic,
-                    "valu_insts": pmc.get("SQ_INSTS_VALU"), "clock_ghz": clock,
+                    "valu_insts": pmc.get("SQ_INSTS_VALU"),
                     "window_vs_bench": s.get("window_vs_bench_event_time")}
 print(json.dumps(summary, indent=1))
