@@ -15,7 +15,7 @@ line also times the RCCL gather of every shard's hashes to rank 0 (shard.gather_
 Every rank's shard is checked against the reference's digests
 (tests/golden/digests.json, fixed32_1G chunks) outside the timed region.
 
-At N = 1 the line also carries secondary results (configs 3, 4 and 5, and the
+At N = 1 the line also carries secondary results (configs 3, 4 and 5, RALLEDATA blobs and the
 host-memory path) and a CPU baseline: the reference's own hash path (oracle/_ref),
 timed on this host's cores.
 
@@ -366,6 +366,40 @@ def secondary_fixed(name, dev, steps, warm_ms, verify, golden_name):
     return res
 
 
+def secondary_ralledata(dev, steps, warm_ms, verify):
+    """RALLEDATA blobs (hash + subhash + lengths + key + value) for bench's
+    ralledata workload, one kernel per call; checked against tests/golden/ralledata_digest.json
+    (the oracle's layout restatement over the reference-pinned hash)."""
+    import torch
+
+    from k2hash_amd import batch, ralledata
+
+    _, n, ((klo, khi), (vlo, vhi)), desc = CONFIGS["ralledata"]
+    ko = batch.synth_offsets(n, dev, klo, khi)
+    vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7)
+    kb, vb = int(ko[-1].item()), int(vo[-1].item())
+    kd = batch.synth_bytes(kb, dev)
+    vd = batch.synth_bytes(vb, dev, byte_off=1 << 33)
+    total = 80 * n + kb + vb
+    blob = torch.zeros((total + 7) // 8 * 8, dtype=torch.uint8, device=dev)  # zero pad: digest over u64 words
+    boff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    wall, kern, _ = timed(lambda i: ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff, total=total),
+                          steps, 3, warm_ms)
+    algo = (kb + vb + 16 * (n + 1)) + (total + 8 * (n + 1))
+    model = sum(chunks_of(L) for L in range(klo, khi + 1)) / (khi - klo + 1) * FNV_OPS_PER_CHUNK * n / 64
+    res = {"workload": desc, "records": n, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
+           "value": n * steps / wall, "unit": "records/s", "blob_gb_per_s": total * steps / wall / 1e9,
+           "roofline": roofline("ralledata", algo, kern, model)}
+    if verify:
+        g = json.loads((ROOT / "tests" / "golden" / "ralledata_digest.json").read_text())
+        ok = g["n"] == n and g["bytes"] == total and digest_dev(blob.view(torch.int64), 0) == g["blob"] and \
+            digest_dev(boff, 0) == g["blob_off"]
+        res["verify"] = {"ok": ok, "against": "tests/golden/ralledata_digest.json"}
+    del ko, vo, kd, vd, blob, boff
+    torch.cuda.empty_cache()
+    return res
+
+
 def secondary_host(dev, reps=5):
     """Host-memory path (PCIe-inclusive; never `value`): keys in pageable host memory ->
     k2h_amd_hash_*_host -> hashes in host memory.  16M x 32 B fixed keys, and 8M CSR keys
@@ -631,6 +665,7 @@ def main():
                 "csr": secondary_csr(dev, 20, 60.0, vf),
                 "fixed4096": secondary_fixed("fixed4096", dev, 20, 60.0, vf, "fixed4096_1M"),
                 "fixed32_1g": secondary_fixed("fixed32_1g", dev, 10, 60.0, vf, "fixed32_1G"),
+                "ralledata": secondary_ralledata(dev, 20, 60.0, vf),
                 "host": secondary_host(dev),
             }
         if not args.no_cpu_baseline:

@@ -328,7 +328,7 @@ enum {
   kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
   kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10,
   kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13, kModeLean2Group = 14,
-  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22
+  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -860,7 +860,9 @@ __device__ __forceinline__ void pair_walk2(uint32_t k0, uint32_t p0, const uint8
   }
 }
 
-template <bool H2, bool EPI = false, int WALK = 0>
+// CLK (lab clock probe, H2 false): h2 receives per wave the shader-clock / 100 MHz stamps
+// at entry and after the hash (tools/clock_probe.py)
+template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false>
 __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
                                                             SpadTable spad_tab, uint64_t* __restrict__ h1,
@@ -876,6 +878,11 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
   __shared__ uint4 s_mask[16];
   __shared__ __attribute__((aligned(16))) uint8_t s_stage[16 + kStage];
 
+  uint64_t clk0 = 0, rt0 = 0;
+  if constexpr (CLK) {
+    clk0 = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t t0 = (uint64_t)blockIdx.x * TK;
@@ -976,6 +983,16 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
       h1[t0 + kbi] = hB;
       if constexpr (H2) h2[t0 + kbi] = second_from_first(hB, lb, key0 + rbe);
       if constexpr (EPI) bucket_emit<false>(bp, t0 + kbi, hB);
+    }
+    if constexpr (CLK) {
+      const uint64_t clk1 = __builtin_amdgcn_s_memtime(), rt1 = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) {
+        uint64_t* o = h2 + 4ull * (blockIdx.x * NW + wave);
+        o[0] = clk0;
+        o[1] = clk1;
+        o[2] = rt0;
+        o[3] = rt1;
+      }
     }
     return;
   }
@@ -1426,6 +1443,21 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModePair4W2) return launch_pair<4, 72, false, false, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair4PS) return launch_pair<4, 72, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair2PS) return launch_pair<2, 36, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModeLean2Clock) {  // h2 = stamp buffer (4 words per wave), tiles past the stage not hashed
+    if (!h2) return hipErrorInvalidValue;
+    const unsigned gc = (unsigned)((n + kTileKeys - 1) / kTileKeys);
+    uint32_t* scratch = nullptr;
+    hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (gc + 1), stream);
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(scratch, 0, 4, stream);
+    if (e == hipSuccess) {
+      fnv_csr_lean2_kernel<false, false, 3, true><<<gc, 256, 0, stream>>>((const uint8_t*)bytes, offsets, n, t, h1, h2,
+                                                                         scratch + 1, scratch);
+      e = hipGetLastError();
+    }
+    hipError_t f = hipFreeAsync(scratch, stream);
+    return e != hipSuccess ? e : f;
+  }
   unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
   const uint8_t* b = (const uint8_t*)bytes;
   if (mode == kModeLeanRing || mode == kModeLean2Ring || mode == kModeLean2Pin || mode == kModeLean2Step ||

@@ -91,6 +91,7 @@ enum {
   kVariantLongHalf2 = 70,         // fixed long keys: 2 half-line rounds (8 KiB ring per wave)
   kVariantFixed32Clock = 71,      // clock probes: the default fixed32 / 4 KiB kernels, h2 = per-wave stamps of the
   kVariantLongClock = 72,         // shader clock (s_memtime) and the 100 MHz counter (tools/clock_probe.py)
+  kVariantCsrClock = 78,         // clock probe: the default CSR kernel (lean2), h2 = per-wave stamps (H2 off)
   kVariantRalleGroup8 = 73,       // ralledata: the round-1/2 group kernel (8 lanes per record, unaligned stores)
   kVariantRalleGather = 74,       // ralledata: output-driven gather from LDS-staged segments (aligned line stores)
   kVariantRalleGatherFused = 75,  // ... with the key hashes computed in the same kernel from the staged keys (default)

@@ -825,6 +825,7 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrPair2PS ? 20
                          : variant == kVariantCsrPair4W2 ? 21
                          : variant == kVariantCsrPair4Z ? 22
+                         : variant == kVariantCsrClock ? 23
                                                         : 11,
                          stream, epi ? bp : nullptr);
 }

@@ -24,7 +24,7 @@ import torch  # noqa: E402
 import k2hash_amd  # noqa: E402
 from k2hash_amd import _native, batch  # noqa: E402
 
-CASES = {"fixed32": (32, 1 << 24, 71), "fixed4096": (4096, 1 << 20, 72)}
+CASES = {"fixed32": (32, 1 << 24, 71), "fixed4096": (4096, 1 << 20, 72), "csr": (None, 1 << 26, 78)}
 
 p = argparse.ArgumentParser()
 p.add_argument("--warm", type=int, default=200, help="product launches before the probe (clock ramp)")
@@ -34,19 +34,25 @@ a = p.parse_args()
 dev = torch.device("cuda:0")
 res = {}
 for name, (L, n, var) in CASES.items():
-    keys = batch.synth_bytes(n * L, dev)
+    if L is None:  # BASELINE config 3: CSR keys of 8-256 B
+        off = batch.synth_offsets(n, dev, 8, 256)
+        keys = batch.synth_bytes(int(off[-1].item()), dev)
+        hash_ = lambda out: k2hash_amd.hash_csr(keys, off, out=out)  # noqa: E731
+    else:
+        keys = batch.synth_bytes(n * L, dev)
+        hash_ = lambda out: k2hash_amd.hash_fixed(keys, L, out=out)  # noqa: E731
     h1 = torch.empty(n, dtype=torch.int64, device=dev)
-    ref, _ = k2hash_amd.hash_fixed(keys, L)
     _native.lab_set_variant(0)
+    ref, _ = hash_(None)
     for _ in range(a.warm):
-        k2hash_amd.hash_fixed(keys, L, out=(h1, None))
+        hash_((h1, None))
     _native.lab_set_variant(var)
     rows = []
     for _ in range(a.reps):
         st = torch.zeros(n, dtype=torch.int64, device=dev)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
-        k2hash_amd.hash_fixed(keys, L, out=(h1, st))
+        hash_((h1, st))
         ev1.record()
         torch.cuda.synchronize()
         s = st.view(-1, 4)
@@ -59,6 +65,7 @@ for name, (L, n, var) in CASES.items():
                      "span_us": round(span_us, 2), "event_us": round(ev0.elapsed_time(ev1) * 1e3, 2)})
     _native.lab_set_variant(0)
     ok = torch.equal(h1, ref)
+    del keys
     res[name] = {"hashes_match": ok, "reps": rows,
                  "clock_ghz": round(sum(r["clock_ghz"] for r in rows[1:]) / max(1, len(rows) - 1), 4)}
     print(name, json.dumps(res[name]), flush=True)
