@@ -97,6 +97,8 @@ enum {
   kVariantRalleGatherFused = 75,  // ... with the key hashes computed in the same kernel from the staged keys (default)
   kVariantRallePhases = 76,       // the one-shot gather form with per-block phase stamps in blob_off (tools/ralle_phases.py)
   kVariantRallePhasesNoStore = 77,  // ... and no piece stores (timing probe, wrong blobs)
+  kVariantRallePieces2 = 79,      // gather form, two output pieces per loop trip
+  kVariantRalleStageAll = 80,     // gather form, staged loads on all four waves
   kVariantCsrPair4Z = 69,         // csr pair tiles (512 keys), the mad64 zero half kept in v50 across the walk
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)

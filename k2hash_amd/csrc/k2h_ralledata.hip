@@ -245,8 +245,11 @@ __device__ __forceinline__ void staged_key_hash(const uint8_t* end, uint32_t len
 // scratch); otherwise h holds h1[n] then h2[n] from the CSR hash kernel.  PROBE (lab,
 // tools/ralle_phases.py): thread 0 overwrites blob_off[r0 .. r0+4] with shader-clock
 // stamps at entry, after each barrier and at the end of its pieces (wrong offsets).
-template <bool FUSED, int PROBE = 0>  // PROBE 1: stamps, 2: stamps + no piece stores (timing only)
-__global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
+// PROBE 1: stamps, 2: stamps + no piece stores (timing only); PU: pieces per loop trip;
+// SW0: the staged loads on all four waves (default: waves 1-3, so wave 0 only waits for its
+// records' offsets)
+template <bool FUSED, int PROBE = 0, int PU = 1, bool SW0 = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void ralledata_gather_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
                                                                uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off,
                                                                SpadTable spad_tab) {
   constexpr int R = kGatherRecs, NSEG = 5 * R;
@@ -257,12 +260,21 @@ __global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, u
   __shared__ u32x4_al qmask[17];
   __shared__ uint64_t spad[16];
   const uint32_t tid = threadIdx.x;
-  uint64_t t0 = 0, t1 = 0, t2 = 0;
+  uint64_t t0 = 0, t1 = 0, t2 = 0, ta = 0, tb = 0;
   if constexpr (PROBE) t0 = __builtin_amdgcn_s_memtime();
   const uint64_t r0 = (uint64_t)blockIdx.x * R;
   const uint32_t nr = (uint32_t)(n - r0 < (uint64_t)R ? n - r0 : (uint64_t)R);
   const uint64_t* offs[4] = {in.koff, in.voff, in.soff, in.aoff};
   const uint8_t* srcs[4] = {in.keys, in.vals, in.skeys, in.attrs};
+  // the records' own offsets first: they do not depend on the span offsets below
+  uint32_t ro0[4] = {0, 0, 0, 0}, ro1[4] = {0, 0, 0, 0};
+  if (tid < nr) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ro0[s] = offs[s] ? (uint32_t)offs[s][r0 + tid] : 0u;
+      ro1[s] = offs[s] ? (uint32_t)offs[s][r0 + tid + 1] : 0u;
+    }
+  }
   // block-uniform: each input span, its aligned hull, where it goes in the image
   uint64_t o_first = 80ull * r0, span = 80ull * nr, hull_total = 0;
   uint64_t sbase[4], hull_lo[4], hull_n[4];
@@ -296,15 +308,18 @@ __global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, u
     }
     return;
   }
-  // 1a. the staged pieces: up to 4 aligned loads per thread, issued first
-  constexpr int PPT = (kGatherPool / 16 + 255) / 256;
+  if constexpr (PROBE != 0) ta = __builtin_amdgcn_s_memtime();  // span offsets arrived
+  // 1a. the staged pieces: up to 4 aligned loads per thread of waves 1-3 (wave 0's only
+  // loads are its records' offsets, so its record work waits for nothing else)
+  constexpr uint32_t SW = SW0 ? 0 : 64, NST = 256 - SW;
+  constexpr int PPT = (kGatherPool / 16 + NST - 1) / NST;
   u32x4_al v[PPT];
   uint32_t dst[PPT];
 #pragma unroll
   for (int u = 0; u < PPT; ++u) {
-    uint64_t q = tid + 256u * u;
+    const uint64_t q = (uint64_t)tid - SW + NST * u;
     dst[u] = 0xffffffffu;
-    if (q < hull_total) {
+    if (tid >= SW && q < hull_total) {
       uint64_t addr = 0, before = 0;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -333,9 +348,8 @@ __global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, u
     uint32_t rel[4], len[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const uint32_t o0 = offs[s] ? (uint32_t)offs[s][i] : 0u, o1 = offs[s] ? (uint32_t)offs[s][i + 1] : 0u;
-      rel[s] = o0 - (uint32_t)sbase[s];
-      len[s] = o1 - o0;
+      rel[s] = ro0[s] - (uint32_t)sbase[s];
+      len[s] = ro1[s] - ro0[s];
     }
     const int32_t B = (int32_t)(80u * tid + rel[0] + rel[1] + rel[2] + rel[3]);
     const uint32_t kl = len[0], vl = len[1], sl = len[2], al = len[3];
@@ -366,6 +380,7 @@ __global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, u
       if (i + 1 == n) blob_off[n] = o_first + start;
     }
   }
+  if constexpr (PROBE != 0) tb = __builtin_amdgcn_s_memtime();  // records done (thread 0)
 #pragma unroll
   for (int u = 0; u < PPT; ++u)
     if (dst[u] != 0xffffffffu) *reinterpret_cast<u32x4_al*>(img + dst[u]) = v[u];
@@ -373,8 +388,7 @@ __global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, u
   if constexpr (PROBE) t1 = __builtin_amdgcn_s_memtime();
   if constexpr (FUSED) {  // 1c. wave 0 hashes the block's keys from the image into the headers
     if (tid < nr) {
-      const uint32_t kl = in.koff ? (uint32_t)in.koff[r0 + tid + 1] - (uint32_t)in.koff[r0 + tid] : 0u;
-      const uint32_t ke = in.koff ? (uint32_t)in.koff[r0 + tid + 1] - (uint32_t)sbase[0] : 0u;
+      const uint32_t kl = ro1[0] - ro0[0], ke = ro1[0] - (uint32_t)sbase[0];
       uint64_t h1, h2;
       staged_key_hash(img + area[0] + ke, kl, spad, h1, h2);
       *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid) =
@@ -388,13 +402,10 @@ __global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, u
   const int32_t sp = (int32_t)span;
   const uint32_t np = (uint32_t)((d0 + sp + 15) >> 4);
   uint8_t* const base = out + (o_first - (uint64_t)d0);
-  for (uint32_t p = tid; p < np; p += 256) {
+  // piece p: its first segment s0 (= seg[g]) and the next s1, both windows already read;
+  // further segments (a short or empty one between) are read here
+  auto piece = [&](uint32_t p, uint32_t g, int2 s0, int2 s1, const u32x4_ua& w0, const u32x4_ua& w1) {
     const int32_t x = 16 * (int32_t)p - d0, end = min(x + 16, sp);
-    uint32_t g = tab[p];
-    // the piece's segment and the next one in one read, both windows read together
-    const int2 s0 = seg[g], s1 = seg[g + 1];
-    const u32x4_ua w0 = *reinterpret_cast<const u32x4_ua*>(img + s0.x + x);
-    const u32x4_ua w1 = *reinterpret_cast<const u32x4_ua*>(img + s1.x + x);
     u32x4_al acc = {w0.x, w0.y, w0.z, w0.w};
     int32_t pos = s0.y;
     auto merge = [&](const u32x4_ua& w) {  // bytes [pos - x, 16) from w
@@ -410,7 +421,7 @@ __global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, u
         pos = s1.y;
       }
       ++g;
-      while (pos < end) {  // a third segment starts in this piece (a short or empty one between)
+      while (pos < end) {
         const int2 sn = seg[++g];
         if (sn.y > pos) {
           merge(*reinterpret_cast<const u32x4_ua*>(img + sn.x + x));
@@ -426,14 +437,35 @@ __global__ __launch_bounds__(256) void ralledata_gather_kernel(RalleInputs in, u
       const uint32_t wv[4] = {acc.x, acc.y, acc.z, acc.w};
       for (int k = max(0, -x); k < 16 && x + k < sp; ++k) base[16ull * p + k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
     }
+  };
+  auto window = [&](int2 sg, uint32_t p) {
+    return *reinterpret_cast<const u32x4_ua*>(img + sg.x + 16 * (int32_t)p - d0);
+  };
+  if constexpr (PU == 2) {  // two pieces per trip: their LDS reads in flight together
+    for (uint32_t p = tid; p < np; p += 512) {
+      const uint32_t q = p + 256 < np ? p + 256 : p;
+      const uint32_t ga = tab[p], gb = tab[q];
+      const int2 a0 = seg[ga], a1 = seg[ga + 1], b0 = seg[gb], b1 = seg[gb + 1];
+      const u32x4_ua wa0 = window(a0, p), wa1 = window(a1, p), wb0 = window(b0, q), wb1 = window(b1, q);
+      piece(p, ga, a0, a1, wa0, wa1);
+      if (q != p) piece(q, gb, b0, b1, wb0, wb1);
+    }
+  } else {
+    for (uint32_t p = tid; p < np; p += 256) {
+      const uint32_t g = tab[p];
+      const int2 s0 = seg[g], s1 = seg[g + 1];  // the piece's segment and the next, one read
+      piece(p, g, s0, s1, window(s0, p), window(s1, p));
+    }
   }
   if constexpr (PROBE != 0) {
     const uint64_t t3 = __builtin_amdgcn_s_memtime();
-    if (tid == 0 && nr >= 4) {
+    if (tid == 0 && nr >= 6) {
       blob_off[r0] = t0;
       blob_off[r0 + 1] = t1;
       blob_off[r0 + 2] = t2;
       blob_off[r0 + 3] = t3;
+      blob_off[r0 + 4] = ta;
+      blob_off[r0 + 5] = tb;
     }
   }
 }
@@ -662,6 +694,16 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
   constexpr bool two_kernels = false;
 #endif
 #if K2H_AMD_LAB
+  if (variant == kVariantRalleStageAll) {
+    ralledata_gather_kernel<true, 0, 1, true>
+        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+    return hipGetLastError();
+  }
+  if (variant == kVariantRallePieces2) {
+    ralledata_gather_kernel<true, 0, 2>
+        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+    return hipGetLastError();
+  }
   if (variant == kVariantRallePhasesNoStore) {
     ralledata_gather_kernel<true, 2>
         <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));

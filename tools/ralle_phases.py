@@ -51,9 +51,9 @@ e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1)
 nb = n // 64
-st = boff[:nb * 64].view(nb, 64)[:, :4].double()
-ph = {"stage+records": st[:, 1] - st[:, 0], "hash": st[:, 2] - st[:, 1], "pieces(wave0)": st[:, 3] - st[:, 2],
-      "life(wave0)": st[:, 3] - st[:, 0]}
+st = boff[:nb * 64].view(nb, 64)[:, :6].double()
+ph = {"span offsets": st[:, 4] - st[:, 0], "records (wave 0)": st[:, 5] - st[:, 4], "stage wait + barrier": st[:, 1] - st[:, 5],
+      "hash": st[:, 2] - st[:, 1], "pieces(wave0)": st[:, 3] - st[:, 2], "life(wave0)": st[:, 3] - st[:, 0]}
 res = {"kernel_ms": ms, "blocks": nb}
 for k, v in ph.items():
     res[k] = {"median_cyc": v.median().item(), "mean_cyc": v.mean().item(),
