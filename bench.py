@@ -185,20 +185,28 @@ def cpu_baseline(keys_host, key_len: int, n: int) -> dict | None:
     # thread on 21-byte "KEY-%016X" keys; per-thread timing like tests/k2hbench.cc:937-976
     kb1 = min(lib.cpu_bench_k2hbench(so.encode(), 100000, 100000, 1, ctypes.byref(dig)) for _ in range(3))
     kbN = min(lib.cpu_bench_k2hbench(so.encode(), 100000, 100000, cores, ctypes.byref(dig)) for _ in range(3))
+    nall = info["nproc"] or cores
+    kbA = min(lib.cpu_bench_k2hbench(so.encode(), 100000, 100000, nall, ctypes.byref(dig)) for _ in range(3)) \
+        if nall != cores else kbN
     if not (t1 and tN):
         return None
+    # the reported value: the faster of the box's CPU share and every listed CPU
+    use_all = bool(tall) and tall < tN
+    threads, t = (nall, tall) if use_all else (cores, tN)
+    kb = {"hash_calls_per_thread": 1000000,
+          "threads_1": {"seconds": kb1, "calls_per_s": 1e6 / kb1 if kb1 > 0 else None},
+          f"threads_{cores}": {"seconds": kbN, "calls_per_s": cores * 1e6 / kbN if kbN > 0 else None}}
+    kb[f"threads_{nall}"] = {"seconds": kbA, "calls_per_s": nall * 1e6 / kbA if kbA > 0 else None}
     return {
-        "value": n / tN, "unit": "key hashes/s", "cores": cores, "kind": kind,
+        "value": n / t, "unit": "key hashes/s", "cores": threads, "kind": kind,
         "sample": f"first {n} keys of the same {key_len}B workload (first {m1} at 1 thread), h1 only, "
-                  f"8 passes per run, best of 3 runs, on {cores} threads (the box's CPU share; reference "
-                  f"lib/k2hashfunc.cc k2h_hash via dlsym)",
+                  f"8 passes per run, best of 3 runs, on {threads} threads (best of the box's {cores}-CPU "
+                  f"share and all {nall} listed CPUs; reference lib/k2hashfunc.cc k2h_hash via dlsym)",
         "single_thread": m1 / t1,
-        "all_listed_cpus": {"threads": info["nproc"], "value": n / tall if tall else None},
+        "cpu_share": {"threads": cores, "value": n / tN},
+        "all_listed_cpus": {"threads": nall, "value": n / tall if tall else None},
         "host": info,
-        "k2hbench_rw_100k": {"hash_calls_per_thread": 1000000,
-                              "threads_1": {"seconds": kb1, "calls_per_s": 1e6 / kb1 if kb1 > 0 else None},
-                              f"threads_{cores}": {"seconds": kbN,
-                                                   "calls_per_s": cores * 1e6 / kbN if kbN > 0 else None}},
+        "k2hbench_rw_100k": kb,
     }
 
 
