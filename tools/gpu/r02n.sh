@@ -9,4 +9,4 @@ timeout -k 10 100 python -u tools/ralle_phases.py --variant 76 > gpurun_out/ph76
 python3 -c "
 import json; d=json.load(open('gpurun_out/ph76b.json'))
 print(round(d['kernel_ms'],3), {k:round(d[k]['mean_us'],2) for k in d if isinstance(d[k],dict)}, round(d['resident_blocks_mean']))"
-timeout -k 10 300 python -u tools/ralle_ab.py --variants 73,0,81
+timeout -k 10 300 python -u tools/ralle_ab.py --variants 73,0,81,0
