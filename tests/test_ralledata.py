@@ -194,3 +194,50 @@ def test_device_gather_form_vs_oracle(cuda, oracle, segments):
     if segments.endswith("unaligned"):
         b = big.cpu().numpy()
         assert not b[:5].any() and not b[5 + total:].any()  # nothing outside the blob span
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 127, 129, 1000])
+@pytest.mark.parametrize("std_fnv", [False, True])
+def test_device_small_batches_and_std_fnv(cuda, oracle, n, std_fnv):
+    """Partial tiles (n not a multiple of 64), a single record, and the std::FNV seed
+    (K2H_AMD_FLAG_STD_FNV, oracle variant 1) through the fused hash of the gather form."""
+    import torch
+    k, v, s, a = _random_records(oracle, n, "kvs", (0, 65), (0, 201), seed=n)
+    ref, rboff = oracle.build_ralledata(k, v, s, a, variant=1 if std_fnv else 0)
+    segs = []
+    for x in (k, v, s, a):
+        segs += list(_dev(torch, cuda, x)) if x is not None else [None, None]
+    out, boff = ralledata.build_ralledata(*segs, std_fnv=std_fnv)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert np.array_equal(boff.cpu().numpy().view(np.uint64), rboff)
+
+
+@pytest.mark.gpu
+def test_device_stage_boundary(cuda, oracle):
+    """Tiles whose staged spans sit right at the 12 KiB stage limit, on both sides: 64
+    records per tile with values sized so a tile's key + value hull is 12288 +- 32 bytes;
+    the tiles that do not fit take the group form in the same kernel."""
+    import torch
+    n = 64 * 40
+    k, v = [], []
+    data = oracle.gen_bytes(n * 300, byte_off=5)
+    pos = 0
+    for t in range(40):
+        target = 12288 + (t % 5 - 2) * 16  # key + value bytes of the tile
+        per = target // 64
+        for j in range(64):
+            kl = 8 + (j * 7 + t) % 24
+            vl = max(0, per - kl + (1 if j < target - per * 64 else 0))
+            k.append(data[pos:pos + kl].tobytes())
+            pos += kl
+            v.append(data[pos:pos + vl].tobytes())
+            pos += vl
+    ref, rboff = oracle.build_ralledata(k, v)
+    kd, ko = _dev(torch, cuda, k)
+    vd, vo = _dev(torch, cuda, v)
+    out, boff = ralledata.build_ralledata(kd, ko, vd, vo)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref)
+    assert np.array_equal(boff.cpu().numpy().view(np.uint64), rboff)
