@@ -15,7 +15,8 @@ line also times the RCCL gather of every shard's hashes to rank 0 (shard.gather_
 Every rank's shard is checked against the reference's digests
 (tests/golden/digests.json, fixed32_1G chunks) outside the timed region.
 
-At N = 1 the line also carries secondary results (configs 3, 4 and 5, RALLEDATA blobs and the
+At N = 1 the line also carries secondary results (configs 3, 4 and 5, config 2 with the fused
+bucket index, RALLEDATA blobs and the
 host-memory path) and a CPU baseline: the reference's own hash path (oracle/_ref),
 timed on this host's cores.
 
@@ -374,6 +375,35 @@ def secondary_fixed(name, dev, steps, warm_ms, verify, golden_name):
     return res
 
 
+def secondary_index(dev, steps, warm_ms, verify):
+    """config 2 with the bucket-index epilogue fused into the hash kernel
+    (kindex / ckindex per key, lib/k2hshm.cc:810-833, 1093); checked against
+    tests/golden/index_digest.json (oracle hash + oracle bucket index)."""
+    import torch
+
+    from k2hash_amd import batch
+
+    _, n, L, desc = CONFIGS["fixed32"]
+    g = json.loads((ROOT / "tests" / "golden" / "index_digest.json").read_text())
+    sets = [batch.synth_bytes(n * L, dev, byte_off=s * n * L) for s in range(2)]  # set 0 = the digest's keys
+    out = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(3)]
+    wall, kern, _ = timed(lambda i: batch.hash_fixed_index(sets[i % 2], L, g["cur_mask"], g["collision_mask"],
+                                                           out=(out[0], None, out[1], out[2])), steps, 3, warm_ms)
+    algo = n * L + 8 * n + 16 * n
+    model = n / 64 * chunks_of(L) * FNV_OPS_PER_CHUNK
+    res = {"workload": desc + " + fused bucket index (cur_mask 2^28-1, collision_mask 0xF)", "keys": n,
+           "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3, "value": n * steps / wall,
+           "unit": "key hashes + bucket positions/s", "roofline": roofline("fixed32_index", algo, kern, model)}
+    if verify:
+        batch.hash_fixed_index(sets[0], L, g["cur_mask"], g["collision_mask"], out=(out[0], None, out[1], out[2]))
+        ok = digest_dev(out[0], 0) == g["h1"] and digest_dev(out[1], 0) == g["kindex"] and \
+            digest_dev(out[2], 0) == g["ckindex"]
+        res["verify"] = {"ok": ok, "against": "tests/golden/index_digest.json"}
+    del sets, out
+    torch.cuda.empty_cache()
+    return res
+
+
 def secondary_ralledata(dev, steps, warm_ms, verify):
     """RALLEDATA blobs (hash + subhash + lengths + key + value) for bench's
     ralledata workload, one kernel per call; checked against tests/golden/ralledata_digest.json
@@ -673,6 +703,7 @@ def main():
                 "csr": secondary_csr(dev, 20, 60.0, vf),
                 "fixed4096": secondary_fixed("fixed4096", dev, 20, 60.0, vf, "fixed4096_1M"),
                 "fixed32_1g": secondary_fixed("fixed32_1g", dev, 10, 60.0, vf, "fixed32_1G"),
+                "fixed32_index": secondary_index(dev, 20, 60.0, vf),
                 "ralledata": secondary_ralledata(dev, 20, 60.0, vf),
                 "host": secondary_host(dev),
             }
