@@ -16,10 +16,11 @@
 //   80 i + sum over segments of (seg_off[i] - seg_off[0])
 // and no scan is needed.
 //
-// Two kernels: the CSR hash kernel (k2h_csr.hip) writes h1/h2 to a stream-ordered
-// scratch buffer, then an assembly kernel writes the blobs (16 lanes per record by
-// default; one thread per record as the A/B variant).  Blob and segment addresses are
-// byte-aligned; the global path handles the unaligned 16-byte accesses.
+// One kernel (ralledata_gather_kernel<true>, below): tiles of 64 records staged in LDS,
+// the keys hashed there, the blobs written as aligned 16-byte pieces; tiles too large to
+// stage run the 8-lane group form inside the same kernel.  The lab build keeps the round-1
+// two-kernel forms (CSR hash into scratch, then a group / thread / LDS-image assembly) as
+// A/B variants.  Blob and segment addresses are byte-aligned.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -243,15 +244,16 @@ __device__ __forceinline__ void staged_key_hash(const uint8_t* end, uint32_t len
 
 // FUSED: the key hashes are computed here from the staged key bytes (no hash kernel, no
 // scratch); otherwise h holds h1[n] then h2[n] from the CSR hash kernel.  PROBE (lab,
-// tools/ralle_phases.py): thread 0 overwrites blob_off[r0 .. r0+4] with shader-clock
-// stamps at entry, after each barrier and at the end of its pieces (wrong offsets).
-// PROBE 1: stamps, 2: stamps + no piece stores (timing only); PU: pieces per loop trip;
+// tools/ralle_phases.py): thread 0 overwrites blob_off[r0 .. r0+5] with shader-clock
+// stamps (entry, span offsets in, records done, after each barrier, end of its pieces;
+// wrong offsets), 2: the same without the piece stores.  PU: pieces per loop trip;
 // SW0: the staged loads on all four waves (default: waves 1-3, so wave 0 only waits for its
 // records' offsets)
 template <bool FUSED, int PROBE = 0, int PU = 1, bool SW0 = false>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void ralledata_gather_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
-                                                               uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off,
-                                                               SpadTable spad_tab) {
+// 7 waves/SIMD (<= 72 VGPRs): the LDS image allows 7 blocks per CU
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void ralledata_gather_kernel(
+    RalleInputs in, uint64_t n, const uint64_t* __restrict__ h, uint8_t* __restrict__ out,
+    uint64_t* __restrict__ blob_off, SpadTable spad_tab) {
   constexpr int R = kGatherRecs, NSEG = 5 * R;
   typedef uint32_t u32x4_al __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) uint8_t img[kGatherImg];
