@@ -54,3 +54,26 @@ def test_bench_n1_headline_verified():
     line = _run(["--steps", "5", "--warmup", "2", "--warm-ms", "10", "--no-secondary", "--no-cpu-baseline"], 600)
     assert line["n_gpus"] == 1 and line["verify"]["ok"] is True
     assert 0 < line["roofline"]["frac"] < 1 and 0 < line["roofline"]["valu_frac"] < 1.2
+
+
+def test_digest_and_chunk_check_match_oracle(oracle):
+    """bench.py's on-device verification (digest_dev / verify_chunks), run on CPU tensors:
+    equal to the oracle's digest, including a chunk that starts at a non-zero global key
+    index, and a chunk outside the shard is skipped, a corrupted one fails."""
+    import numpy as np
+    import torch
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    h = np.random.default_rng(5).integers(0, 2**63, size=10007, dtype=np.int64).view(np.uint64)
+    t = torch.from_numpy(h.view(np.int64).copy())
+    assert bench.digest_dev(t, 0) == [f"{x:016x}" for x in oracle.digest(h)]
+    first = 3000
+    chunks = [dict(first=3000, count=5000, h1=[f"{x:016x}" for x in oracle.digest(h[3000:8000], 3000)]),
+              dict(first=0, count=100, h1=["0"] * 3)]  # outside [first, first + n): skipped
+    r = bench.verify_chunks(t[first:], first, chunks)
+    assert r == {"chunks_checked": 1, "ok": True}
+    bad = t[first:].clone()
+    bad[17] ^= 1
+    assert bench.verify_chunks(bad, first, chunks)["ok"] is False
