@@ -241,3 +241,50 @@ def test_device_stage_boundary(cuda, oracle):
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy(), ref)
     assert np.array_equal(boff.cpu().numpy().view(np.uint64), rboff)
+
+
+@pytest.mark.gpu
+def test_device_fuzz(cuda, oracle):
+    """Seeded fuzz of the device producer: 40 batches with random record counts, segment
+    sets, length ranges (empty segments included), input and output alignments -- every
+    tile edge and piece/segment boundary position the gather form's alignment math meets."""
+    import torch
+    rng = np.random.default_rng(2024)
+    data = oracle.gen_bytes(1 << 21, byte_off=99)
+    for it in range(40):
+        n = int(rng.integers(1, 1500))
+        present = [True] + [bool(rng.integers(0, 2)) for _ in range(3)]
+        hi = [int(rng.integers(1, 80)), int(rng.integers(1, 300)), int(rng.integers(1, 40)), int(rng.integers(1, 40))]
+        segs_b, pos = [], int(rng.integers(0, 1000))
+        for s in range(4):
+            if not present[s]:
+                segs_b.append(None)
+                continue
+            lens = rng.integers(0, hi[s] + 1, n)
+            lens[rng.random(n) < 0.1] = 0
+            parts = []
+            for L in lens:
+                parts.append(data[pos % (len(data) - 400):][:int(L)].tobytes())
+                pos += int(L)
+            segs_b.append(parts)
+        ref, rboff = oracle.build_ralledata(*segs_b)
+        args = []
+        for parts in segs_b:
+            if parts is None:
+                args += [None, None]
+                continue
+            d, o = _dev(torch, cuda, parts)
+            sh = int(rng.integers(0, 16))  # the bytes at a random alignment, offsets shifted to match
+            pad = torch.zeros(d.numel() + sh, dtype=torch.uint8, device=cuda)
+            pad[sh:] = d
+            args += [pad, o + sh]
+        total = len(ref)
+        osh = int(rng.integers(0, 16))
+        big = torch.zeros(total + 32, dtype=torch.uint8, device=cuda)
+        out, boff = ralledata.build_ralledata(*args, out=big[osh:osh + total], total=total)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy()
+        assert np.array_equal(got, ref), f"batch {it}: n={n} segs={present} first diff {int(np.argmax(got != ref))}"
+        assert np.array_equal(boff.cpu().numpy().view(np.uint64), rboff), f"batch {it}"
+        b = big.cpu().numpy()
+        assert not b[:osh].any() and not b[osh + total:].any(), f"batch {it}: bytes outside the span"
