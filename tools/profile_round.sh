@@ -26,6 +26,7 @@ prof() {  # name, args for bench.py
 for cfg in $CONFIGS; do
   case $cfg in
     fixed32) prof fixed32 --no-secondary --no-cpu-baseline ;;
+    fixed32_index) prof fixed32_index --index --no-secondary --no-cpu-baseline ;;
     *) prof "$cfg" --config "$cfg" --steps 20 --warmup 3 --no-cpu-baseline ;;
   esac
   echo "profiled $cfg"
