@@ -198,6 +198,22 @@ def cpu_baseline(keys_host, key_len: int, n: int) -> dict | None:
           "threads_1": {"seconds": kb1, "calls_per_s": 1e6 / kb1 if kb1 > 0 else None},
           f"threads_{cores}": {"seconds": kbN, "calls_per_s": cores * 1e6 / kbN if kbN > 0 else None}}
     kb[f"threads_{nall}"] = {"seconds": kbA, "calls_per_s": nall * 1e6 / kbA if kbA > 0 else None}
+    # the drop-in plugin (this repo's scalar k2h_hash / k2h_second_hash, libk2hfnv_plugin.so)
+    # in the same harness, 1 thread: it must not be slower than the reference it replaces
+    plugin = ROOT / "k2hash_amd" / "lib" / "libk2hfnv_plugin.so"
+    drop_in = None
+    if plugin.exists() and so:
+        d_ref, d_plug = ctypes.c_uint64(), ctypes.c_uint64()
+        tr = min(lib.cpu_bench_fixed(so.encode(), ptr, key_len, m1, 1, 8, 0, ctypes.byref(d_ref)) for _ in range(3)) / 8
+        tp = min(lib.cpu_bench_fixed(str(plugin).encode(), ptr, key_len, m1, 1, 8, 0, ctypes.byref(d_plug))
+                 for _ in range(3)) / 8
+        kr = min(lib.cpu_bench_k2hbench(so.encode(), 100000, 100000, 1, ctypes.byref(d_ref)) for _ in range(3))
+        kp = min(lib.cpu_bench_k2hbench(str(plugin).encode(), 100000, 100000, 1, ctypes.byref(d_plug))
+                 for _ in range(3))
+        drop_in = {"library": "k2hash_amd/lib/libk2hfnv_plugin.so", "threads": 1,
+                   f"fixed{key_len}_keys_per_s": {"plugin": m1 / tp, "reference": m1 / tr},
+                   "k2hbench_rw_calls_per_s": {"plugin": 1e6 / kp, "reference": 1e6 / kr},
+                   "k2hbench_digest_equal": d_ref.value == d_plug.value}
     return {
         "value": n / t, "unit": "key hashes/s", "cores": threads, "kind": kind,
         "sample": f"first {n} keys of the same {key_len}B workload (first {m1} at 1 thread), h1 only, "
@@ -208,6 +224,7 @@ def cpu_baseline(keys_host, key_len: int, n: int) -> dict | None:
         "all_listed_cpus": {"threads": nall, "value": n / tall if tall else None},
         "host": info,
         "k2hbench_rw_100k": kb,
+        "drop_in_plugin": drop_in,
     }
 
 
