@@ -77,3 +77,17 @@ def test_digest_and_chunk_check_match_oracle(oracle):
     bad = t[first:].clone()
     bad[17] ^= 1
     assert bench.verify_chunks(bad, first, chunks)["ok"] is False
+
+
+def test_bench_measures_the_baseline_metric_and_configs():
+    """bench.py's metric string and workloads are BASELINE.json's: config 2 = 16M x 32 B,
+    3 = 64M CSR keys of 8-256 B, 4 = 2^30 x 32 B over the GPUs, 5 = 4 KiB keys (1M)."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    base = json.loads((ROOT / "BASELINE.json").read_text())
+    assert bench.METRIC == base["metric"]
+    assert bench.CONFIGS["fixed32"][1:3] == (1 << 24, 32) and "16M fixed-length 32B" in base["configs"][1]
+    assert bench.CONFIGS["csr"][1:3] == (1 << 26, (8, 256)) and "64M mixed-length keys 8" in base["configs"][2]
+    assert bench.CONFIGS["fixed32_1g"][1] is None and bench.KEYS_1G == 1 << 30 and "1B 32B keys" in base["configs"][3]
+    assert bench.CONFIGS["fixed4096"][1:3] == (1 << 20, 4096) and "4 KiB keys" in base["configs"][4]
