@@ -47,7 +47,7 @@ enum {
   kVariantFixed32Blk512 = 25,
   kVariantFixed32Blk1024 = 26,
   kVariantFixed32Nt256 = 27,   // fixed32: the round-1 default (nt loads/stores, 256-thread blocks)
-  kVariantRalleThread = 28,    // ralledata: one thread per record (default: 16 lanes per record)
+  kVariantRalleThread = 28,    // ralledata: one thread per record (round-1 A/B)
   kVariantFixed32W64Kpt2 = 29, // fixed32: one-wave blocks, 2 / 3 / 4 keys per lane, all loads issued first, nt
   kVariantFixed32W64Kpt3 = 30,
   kVariantFixed32W64Kpt4 = 31,
@@ -68,7 +68,7 @@ enum {
   kVariantLongProbeMemHalf4 = 46,
   kVariantLongLines256 = 47,      // fixed long keys (len % 256 == 0): 2 rounds of 256 B per lane (32 KiB)
   kVariantCsrTile = 48,           // csr: the round-1 default (512-key tile kernel with the ring inside)
-  kVariantRalleGroup16 = 49,      // ralledata: 16 lanes per record (default 8), overlapped 16-byte tails
+  kVariantRalleGroup16 = 49,      // ralledata: 16 lanes per record, overlapped 16-byte tails
   kVariantRalleByteTail = 50,     // ralledata: the round-1 assembly (16 lanes, tails one byte per lane)
   kVariantCsrLeanRing = 51,       // csr: lean 512-key tiles + ring list, before the VALU trims (default: lean2)
   kVariantCsrLean2Pin = 52,       // csr: lean2 group walk with the chunk registers pinned to the asm banks (the pin
