@@ -3,29 +3,18 @@
 // The same records as the host scanner (k2h_import.cc, restating the std::getline loops
 // of tests/k2himport.cc:74-117) for a file that already sits in HBM, without a host pass:
 //
-// TSV (ConvertfromTsv, tests/k2himport.cc:74-89).  A record's key runs from the record
-// start to the first TAB (across newlines), its value from there to the next '\n'.  So a
-// record ends exactly at the newline of every line that holds a TAB, and the lines with
-// no TAB in front of it belong to its key.  Record ends are therefore a per-line
-// predicate and the loop needs no sequential walk: (1) per 16 KiB block, its newline
-// count and its "span state" (newline seen; TAB / NUL / NUL-after-TAB seen since the
-// last newline), scanned across blocks; (2) newline positions in order, and each line's
-// first TAB and first NUL before / after that TAB (keys and values are cut there,
-// c_str()/strlen) written directly, each thread knowing from the scanned state whether
-// an event is the first of its kind in its line; (3) the TAB lines' indices written in
-// order by the same pass (a per-block record count, taken in pass 1 for both possible
-// incoming states, is scanned like the newline count), then one record per TAB line.  The bytes after the last newline form a last line whose
-// value ends at EOF; if it holds no TAB the key getline hits EOF and it is dropped,
-// as is a trailing run of newline-terminated lines with no TAB.
+// TSV (ConvertfromTsv, tests/k2himport.cc:74-89): the getline loop run as its own
+// two-mode machine, scanned over the bytes (see "TSV as the getline loop's own machine"
+// below): two streaming reads of the file, 32 B per record written, keys hashed from LDS.
 // mdbm (ConvertfromMdbm, tests/k2himport.cc:95-117).  Five header lines (the fifth
 // "HEADER=END", checked on the host from the first newline positions), then line
 // pairs; the EOF rules of the host scanner (an empty value after a key line that ends
 // the file with '\n', the previous record's value after a key line that ends at EOF).
-//
-// Traffic: the file is read twice (pass 1: newline count, span state and record-end
-// count per block; pass 2: newline positions, per-line TAB / NUL positions and the
-// record-ending lines, written directly; a count-only TSV call stops after pass 1); outputs are 8 B per
-// line plus 32 B per record.  Every pass is a streaming read.
+// Lines are found by two passes over 16 KiB blocks: (1) per block, its newline count and
+// whether a NUL follows its last newline, scanned across blocks; (2) every newline's
+// position and every line's first NUL (the C-string cut), written directly, each thread
+// knowing from the scanned state whether a NUL is its line's first.  Outputs: 16 B per
+// line plus 32 B per record.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -76,28 +65,20 @@ __device__ inline void load_span(const uint8_t* f, uint64_t size, uint64_t b, ui
   }
 }
 
-struct LineInfo {
-  uint64_t tab;       // first TAB in the line, or kNone
-  uint64_t nul;       // first NUL in the line (anywhere), or kNone
-  uint64_t nul_tab;   // first NUL after the first TAB, or kNone
-};
-
 __device__ inline uint64_t line_begin(const uint64_t* nl, uint64_t j) { return j ? nl[j - 1] + 1 : 0; }
 __device__ inline uint64_t line_end(const uint64_t* nl, uint64_t nnl, uint64_t size, uint64_t j) {
   return j < nnl ? nl[j] : size;
 }
 
-// State of the line that is open at some point of the file, summarised over a span of
-// bytes: whether the span holds a newline, and since its last newline (or its start)
-// whether a TAB, a NUL, and a NUL after a TAB were seen.  Combining spans in file order
-// is associative (a segmented "or"), so blocks and threads get their incoming state
-// from scans: a thread then knows, for every TAB / NUL it holds, whether it is the
-// first of its kind in its line.
-enum : uint32_t { kHasNl = 1, kTab = 2, kNul = 4, kNulTab = 8 };
+// State of the line open at some point of the file, summarised over a span of bytes:
+// whether the span holds a newline, and whether a NUL was seen since its last newline
+// (or its start).  Combining spans in file order is associative (a segmented "or"), so
+// blocks and threads get their incoming state from scans.
+enum : uint32_t { kHasNl = 1, kNul = 2 };
 struct SpanOp {
   __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const {
     if (b & kHasNl) return b;
-    return (a & kHasNl) | ((a | b) & (kTab | kNul | kNulTab)) | (((a & kTab) && (b & kNul)) ? kNulTab : 0);
+    return (a & kHasNl) | ((a | b) & kNul);
   }
 };
 
@@ -114,152 +95,74 @@ __device__ inline uint32_t nl_count(const uint32_t w[16]) {
   return c;
 }
 
-// Walk the span's events in byte order from state `st`; with Write, record each newline
-// position and each line's first TAB / first NUL / first NUL after its first TAB, and
-// (rl != NULL, TSV) the index of every line that ends a record -- a line holding a TAB --
-// at rl[rec++].  Counts the record ends it passes.
-struct Walk {
-  uint32_t st;        // state after the span
-  uint32_t recs;      // newlines that end a TAB line
-  bool first_nl_tab;  // the first newline's line had a TAB (within the span)
-  bool any_nl;
-};
-
+// Walk the span's newlines and NULs in byte order from state `st`; with Write, record
+// each newline position and each line's first NUL.  Returns the state after the span.
 template <bool Write>
-__device__ inline Walk span_walk(const uint32_t w[16], uint64_t b, uint32_t st, uint64_t line,
-                                 uint64_t* __restrict__ nl, LineInfo* __restrict__ info, uint64_t* __restrict__ rl,
-                                 uint64_t rec) {
-  Walk r{st, 0, false, false};
+__device__ inline uint32_t span_walk(const uint32_t w[16], uint64_t b, uint32_t st, uint64_t line,
+                                     uint64_t* __restrict__ nl, uint64_t* __restrict__ lnul) {
 #pragma unroll
   for (int k = 0; k < 16; ++k) {
-    // masks per word, not kept for the span: fewer live registers, more waves
     const uint32_t mnl = eq_mask(w[k], 0x0A0A0A0Au);
-    uint32_t x = mnl | eq_mask(w[k], 0x09090909u) | eq_mask(w[k], 0);
+    uint32_t x = mnl | eq_mask(w[k], 0);
     while (x) {
       const int bit = __builtin_ctz(x);
       x &= x - 1;
       const uint64_t pos = b + 4 * k + (bit >> 3);
       if (mnl & (1u << bit)) {
         if constexpr (Write) nl[line] = pos;
-        if (!r.any_nl) r.first_nl_tab = (st & kTab) != 0;
-        r.any_nl = true;
-        if (st & kTab) {
-          if constexpr (Write) {
-            if (rl) rl[rec++] = line;
-          }
-          ++r.recs;
-        }
         ++line;
         st = kHasNl;
-      } else if (((w[k] >> (bit - 7)) & 0xFFu) == 9) {  // TAB
-        if (!(st & kTab)) {
-          if constexpr (Write) info[line].tab = pos;
-          st |= kTab;
-        }
-      } else {  // NUL
-        if (!(st & kNul)) {
-          if constexpr (Write) info[line].nul = pos;
-          st |= kNul;
-        }
-        if ((st & kTab) && !(st & kNulTab)) {
-          if constexpr (Write) info[line].nul_tab = pos;
-          st |= kNulTab;
-        }
+      } else if (!(st & kNul)) {
+        if constexpr (Write) lnul[line] = pos;
+        st |= kNul;
       }
     }
   }
-  r.st = st;
-  return r;
+  return st;
 }
 
-// Record ends in a span given whether the line open at its start already holds a TAB
-// (only the span's first newline depends on it).
-__device__ inline uint32_t span_recs(const Walk& s, uint32_t in) {
-  return s.recs + ((in & kTab) && s.any_nl && !s.first_nl_tab ? 1u : 0u);
-}
-
-// Pass 1: per block, the newline count, the span state, and the record-end count for
-// both possible incoming states (low / high 32 bits: open line without / with a TAB).
+// Pass 1: per block, the newline count and the span state.
 __global__ __launch_bounds__(kThreads) void span_count_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                               uint64_t* __restrict__ block_cnt,
-                                                              uint32_t* __restrict__ block_state,
-                                                              uint64_t* __restrict__ block_recs) {
+                                                              uint32_t* __restrict__ block_state) {
   const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
-  uint32_t c = 0;
-  Walk s{0, 0, false, false};
+  uint32_t c = 0, st = 0;
   if (b < size) {
     uint32_t w[16];
     load_span(f, size, b, w);
     c = nl_count(w);
-    s = span_walk<false>(w, b, 0, 0, nullptr, nullptr, nullptr, 0);
-  }
-  typedef hipcub::BlockReduce<uint64_t, kThreads> Reduce;
-  typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
-  __shared__ union {
-    typename Reduce::TempStorage r;
-    typename Scan::TempStorage s;
-  } tmp;
-  // incoming state assuming the block starts on a line with no TAB; assuming one with a
-  // TAB differs only before the block's first newline: in1 has kTab iff in0 has, or no
-  // newline precedes the thread
-  uint32_t in0;
-  Scan(tmp.s).ExclusiveScan(s.st, in0, 0u, SpanOp());
-  __syncthreads();
-  const uint32_t in1 = (in0 & kHasNl) ? in0 : (in0 | kTab);
-  // newline count and both record counts fit 21 bits each (<= 16384 per block)
-  const uint64_t packed = (uint64_t)c | ((uint64_t)span_recs(s, in0) << 21) | ((uint64_t)span_recs(s, in1) << 42);
-  const uint64_t sum = Reduce(tmp.r).Sum(packed);
-  if (threadIdx.x == kThreads - 1) block_state[blockIdx.x] = SpanOp()(in0, s.st);
-  if (threadIdx.x == 0) {
-    constexpr uint64_t m21 = (1ull << 21) - 1;
-    block_cnt[blockIdx.x] = sum & m21;
-    block_recs[blockIdx.x] = ((sum >> 21) & m21) | (((sum >> 42) & m21) << 32);
-  }
-}
-
-// Record-end count of each block under its real incoming state.
-__global__ __launch_bounds__(kThreads) void block_recs_kernel(const uint64_t* __restrict__ both,
-                                                              const uint32_t* __restrict__ block_in, uint64_t nblk,
-                                                              uint64_t* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= nblk) return;
-  out[i] = (block_in[i] & kTab) ? both[i] >> 32 : both[i] & 0xFFFFFFFFu;
-}
-
-// Pass 2 (block_base / block_in / rec_base = exclusive scans of pass 1): newline
-// positions in order, every line's first TAB / NUL / NUL-after-TAB written straight
-// into info, and (TSV) the record-ending line indices into rl -- including the bytes
-// after the last newline when they hold a TAB (a record whose value ends at EOF).
-__global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                              const uint64_t* __restrict__ block_base,
-                                                              const uint32_t* __restrict__ block_in,
-                                                              const uint64_t* __restrict__ rec_base,
-                                                              uint64_t* __restrict__ nl,
-                                                              LineInfo* __restrict__ info,
-                                                              uint64_t* __restrict__ rl) {
-  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
-  uint32_t w[16];
-  uint32_t c = 0;
-  Walk s{0, 0, false, false};
-  if (b < size) {
-    load_span(f, size, b, w);
-    c = nl_count(w);
-    s = span_walk<false>(w, b, 0, 0, nullptr, nullptr, nullptr, 0);
+    st = span_walk<false>(w, b, 0, 0, nullptr, nullptr);
   }
   typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
   __shared__ typename Scan::TempStorage tmp;
-  // newline count (<= 2^14 per block) above the 4 state bits: one scan for both
-  uint32_t co, ro;
-  Scan(tmp).ExclusiveScan((c << 8) | s.st, co, block_in[blockIdx.x], CountStateOp());
-  __syncthreads();
-  const uint32_t o = co >> 8, in = co & 0xFFu;
-  Scan(tmp).ExclusiveSum(span_recs(s, in), ro);
+  uint32_t inc;
+  Scan(tmp).InclusiveScan((c << 8) | st, inc, CountStateOp());  // <= 2^14 newlines per block
+  if (threadIdx.x == kThreads - 1) {
+    block_cnt[blockIdx.x] = inc >> 8;
+    block_state[blockIdx.x] = inc & 0xFFu;
+  }
+}
+
+// Pass 2 (block_base / block_in = exclusive scans of pass 1): newline positions in order
+// and every line's first NUL.
+__global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                              const uint64_t* __restrict__ block_base,
+                                                              const uint32_t* __restrict__ block_in,
+                                                              uint64_t* __restrict__ nl, uint64_t* __restrict__ lnul) {
+  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
+  uint32_t w[16];
+  uint32_t c = 0, st = 0;
+  if (b < size) {
+    load_span(f, size, b, w);
+    c = nl_count(w);
+    st = span_walk<false>(w, b, 0, 0, nullptr, nullptr);
+  }
+  typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  uint32_t co;
+  Scan(tmp).ExclusiveScan((c << 8) | st, co, block_in[blockIdx.x], CountStateOp());
   if (b >= size) return;
-  const uint64_t line = block_base[blockIdx.x] + o, rec = rec_base[blockIdx.x] + ro;
-  const Walk e = span_walk<true>(w, b, in, line, nl, info, rl, rec);
-  // the thread holding the last byte: an open last line with a TAB is a record
-  if (rl && b + kBytesPerThread >= size && f[size - 1] != '\n' && (e.st & kTab))
-    rl[rec + e.recs] = line + c;
+  span_walk<true>(w, b, co & 0xFFu, block_base[blockIdx.x] + (co >> 8), nl, lnul);
 }
 
 // One lane per record: the key straight from the file (no gather) as k = ceil(len/16)
@@ -318,58 +221,9 @@ __global__ __launch_bounds__(kThreads) void import_hash_kernel(const uint8_t* __
   if (h2) h2[i] = b;
 }
 
-// TSV: record r ends at TAB line rl[r]; its key starts after the previous TAB line.
-// nul_from[k] = the first line j >= nlines - 1 - k whose bytes hold a NUL (kNone if none):
-// a min-scan over the lines in reverse order, so a record whose key spans many TAB-less
-// lines cuts it at its first NUL in O(1) (one lane used to walk those lines).
-struct NulLineRev {
-  const LineInfo* info;
-  uint64_t nlines;
-  __host__ __device__ uint64_t operator()(uint64_t k) const {
-    const uint64_t j = nlines - 1 - k;
-    return info[j].nul != kNone ? j : kNone;
-  }
-};
-struct MinOp {
-  __host__ __device__ uint64_t operator()(uint64_t a, uint64_t b) const { return a < b ? a : b; }
-};
-
-__global__ __launch_bounds__(kThreads) void tsv_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
-                                                               uint64_t size, const LineInfo* __restrict__ info,
-                                                               const uint64_t* __restrict__ nul_from, uint64_t nlines,
-                                                               const uint64_t* __restrict__ rl, uint64_t nrec,
-                                                               k2h_amd_import_rec* __restrict__ recs,
-                                                               const uint8_t* __restrict__ f, SpadTable sp,
-                                                               uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
-  const uint64_t r = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (r >= nrec) return;
-  const uint64_t j1 = rl[r], j0 = r ? rl[r - 1] + 1 : 0;
-  const uint64_t kb = line_begin(nl, j0);
-  const LineInfo L = info[j1];
-  uint64_t kend = L.tab;
-  if (j1 > j0) {  // key lines before the TAB line (usually none): the first NUL in them, O(1)
-    const uint64_t jn = nul_from[nlines - 1 - j0];  // first line >= j0 holding a NUL
-    if (jn < j1) kend = info[jn].nul;
-  }
-  if (kend == L.tab && L.nul != kNone && L.nul < L.tab) kend = L.nul;
-  const uint64_t vb = L.tab + 1, ve = L.nul_tab != kNone ? L.nul_tab : line_end(nl, nnl, size, j1);
-  k2h_amd_import_rec o;
-  o.key_off = kb;
-  o.key_len = kend - kb;
-  o.val_off = vb;
-  o.val_len = ve - vb;  // a TAB that ends the file: getline fails, empty value at EOF
-  recs[r] = o;
-  if (h1) {  // fused prehash: the key as the C string Set stores
-    uint64_t a, b;
-    hash_cstr(f, o.key_off, o.key_len, sp, a, b);
-    h1[r] = a;
-    if (h2) h2[r] = b;
-  }
-}
-
 // mdbm: key line 5 + 2r, value line 6 + 2r (see the header comment for the EOF rules).
 __global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
-                                                                uint64_t size, const LineInfo* __restrict__ info,
+                                                                uint64_t size, const uint64_t* __restrict__ lnul,
                                                                 uint64_t nlines, uint64_t nrec, uint64_t body,
                                                                 k2h_amd_import_rec* __restrict__ recs,
                                                                 const uint8_t* __restrict__ f, SpadTable sp,
@@ -379,7 +233,7 @@ __global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* 
   const uint64_t kl = 5 + 2 * r;
   auto cut = [&](uint64_t j) {  // strlen of line j's C string
     const uint64_t b = line_begin(nl, j), e = line_end(nl, nnl, size, j);
-    return (info[j].nul != kNone ? info[j].nul : e) - b;
+    return (lnul[j] != kNone ? lnul[j] : e) - b;
   };
   k2h_amd_import_rec o;
   o.key_off = line_begin(nl, kl);
@@ -411,15 +265,331 @@ __global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* 
 
 unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
 
+// ---------------------------------------------------------------------------
+// TSV as the getline loop's own machine (round 2).  ConvertfromTsv
+// (tests/k2himport.cc:78-86) alternates getline(key, '\t') and getline(value): mode K
+// reads a key up to its TAB (newlines included), mode V a value up to its newline (TABs
+// included).  A record ends at every newline read in mode V, and one more at EOF if the
+// file stops in mode V (the value getline hits EOF after the key's TAB); a key getline
+// that hits EOF drops its bytes.  Set stores C strings (lib/k2hshm.cc:2081-2083), so a
+// field is cut at its first NUL: a NUL is its field's first iff the last NUL before it
+// lies before the field's start.  A span of bytes therefore acts on the state (mode,
+// record index, field start, last NUL) as a small function: per entry mode, the exit
+// mode, the record ends passed and the last field boundary (a TAB read in K, a newline
+// read in V); plus its last NUL.  These functions compose associatively (positions only
+// grow, so "last" combines with max), so each 16 KiB block gets its entry state from a
+// device scan of block functions and each thread from a block scan of 3-word functions
+// of its 128 bytes.  The thread then walks its bytes' events and writes every field at
+// its end event -- key (off, len) at the key's first NUL or else its TAB, value (off,
+// len) at the value's first NUL or else its newline (or EOF) -- and lists the keys that
+// end in its span; the block hashes its list from LDS.  The file is read twice (pass A:
+// block functions; pass B: the walk), and only the 32-byte records and the hashes are
+// written: no per-line arrays.
+// ---------------------------------------------------------------------------
+constexpr int kTThreads = 128;
+constexpr int kTBytes = 128;                                    // bytes per thread
+constexpr uint64_t kTChunk = (uint64_t)kTThreads * kTBytes;     // 16 KiB per block
+constexpr int kTKeys = 256;                                     // LDS key list per block
+
+// Block-local function of a span; positions are block-relative + 1 (0: none).
+//   a: bit 0 / 1 = exit mode entering K / V (1 = V); bits [2, 17) / [17, 32) = record ends
+//      passed entering K / V;  b: last boundary entering K (low half) / V (high half);
+//   c: last NUL.
+struct LFn {
+  uint32_t a, b, c;
+};
+__device__ inline LFn lfn_id() { return LFn{2u, 0u, 0u}; }
+struct LCompose {  // x, then y
+  __device__ LFn operator()(const LFn& x, const LFn& y) const {
+    const uint32_t mk = x.a & 1u, mv = (x.a >> 1) & 1u;  // mode after x, entered in K / V
+    const uint32_t yc0 = (y.a >> 2) & 0x7FFFu, yc1 = y.a >> 17;
+    const uint32_t ck = ((x.a >> 2) & 0x7FFFu) + (mk ? yc1 : yc0), cv = (x.a >> 17) + (mv ? yc1 : yc0);
+    const uint32_t yl0 = y.b & 0xFFFFu, yl1 = y.b >> 16;
+    const uint32_t lk = max(x.b & 0xFFFFu, mk ? yl1 : yl0), lv = max(x.b >> 16, mv ? yl1 : yl0);
+    LFn r;
+    r.a = ((y.a >> mk) & 1u) | (((y.a >> mv) & 1u) << 1) | (ck << 2) | (cv << 17);
+    r.b = lk | (lv << 16);
+    r.c = max(x.c, y.c);
+    return r;
+  }
+};
+
+// The same function over the whole file (absolute positions + 1, 0: none).
+struct alignas(16) GFn {
+  uint32_t map, pad;
+  uint64_t cnt0, cnt1, last0, last1, lnul;
+};
+__host__ __device__ inline GFn gfn_id() { return GFn{2u, 0u, 0, 0, 0, 0, 0}; }
+struct GCompose {
+  __host__ __device__ GFn operator()(const GFn& x, const GFn& y) const {
+    const uint32_t mk = x.map & 1u, mv = (x.map >> 1) & 1u;
+    GFn r;
+    r.map = ((y.map >> mk) & 1u) | (((y.map >> mv) & 1u) << 1);
+    r.pad = 0;
+    r.cnt0 = x.cnt0 + (mk ? y.cnt1 : y.cnt0);
+    r.cnt1 = x.cnt1 + (mv ? y.cnt1 : y.cnt0);
+    const uint64_t yk = mk ? y.last1 : y.last0, yv = mv ? y.last1 : y.last0;
+    r.last0 = x.last0 > yk ? x.last0 : yk;
+    r.last1 = x.last1 > yv ? x.last1 : yv;
+    r.lnul = x.lnul > y.lnul ? x.lnul : y.lnul;
+    return r;
+  }
+};
+__device__ inline GFn gfn_of(const LFn& l, uint64_t base) {
+  GFn g;
+  g.map = l.a & 3u;
+  g.pad = 0;
+  g.cnt0 = (l.a >> 2) & 0x7FFFu;
+  g.cnt1 = l.a >> 17;
+  g.last0 = (l.b & 0xFFFFu) ? base + (l.b & 0xFFFFu) : 0;
+  g.last1 = (l.b >> 16) ? base + (l.b >> 16) : 0;
+  g.lnul = l.c ? base + l.c : 0;
+  return g;
+}
+
+struct TState {
+  uint32_t m;   // mode (1 = V)
+  uint64_t r;   // record being read
+  uint64_t fs;  // its current field's start
+  uint64_t ln;  // last NUL position + 1 (0: none)
+};
+__device__ inline TState gapply(const GFn& g, const TState& s) {
+  TState t;
+  t.m = (g.map >> s.m) & 1u;
+  t.r = s.r + (s.m ? g.cnt1 : g.cnt0);
+  const uint64_t l = s.m ? g.last1 : g.last0;
+  t.fs = l ? l : s.fs;  // the boundary's position + 1 = the next field's start
+  t.ln = s.ln > g.lnul ? s.ln : g.lnul;
+  return t;
+}
+
+// Stage block `blk` into lds[16 .. 16 + 16 KiB) with coalesced 16-byte loads (bytes past
+// the file read as 0x01, no event; the 16 bytes below are chunk 0's pad for the hashes).
+__device__ inline void tsv_stage(const uint8_t* __restrict__ f, uint64_t size, uint64_t blk, uint8_t* lds) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const uint64_t base = blk * kTChunk;
+  const bool aligned = (((uintptr_t)(f + base)) & 15) == 0;
+#pragma unroll
+  for (int q = 0; q < (int)(kTChunk / 16 / kTThreads); ++q) {
+    const uint32_t piece = threadIdx.x + kTThreads * q;
+    const uint64_t o = base + 16ull * piece;
+    u32x4 v;
+    if (aligned && o + 16 <= size) {
+      v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(f + o));
+    } else {
+      uint32_t x[4];
+      for (int k = 0; k < 4; ++k) {
+        x[k] = 0x01010101u;
+        for (int j = 0; j < 4; ++j) {
+          const uint64_t i = o + 4 * k + j;
+          if (i < size) x[k] = (x[k] & ~(0xFFu << (8 * j))) | ((uint32_t)f[i] << (8 * j));
+        }
+      }
+      v = u32x4{x[0], x[1], x[2], x[3]};
+    }
+    *reinterpret_cast<u32x4*>(lds + 16 + 16 * piece) = v;
+  }
+  __syncthreads();
+}
+
+// Candidate event bytes (value < 0x0B: NUL, TAB, newline and the rare 0x01-0x08) of the
+// thread's 128 bytes as two 64-bit masks, one bit per byte.
+__device__ inline void tsv_events(const uint8_t* span, uint64_t& m0, uint64_t& m1) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  uint32_t nib[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const u32x4 v = *reinterpret_cast<const u32x4*>(span + 16 * q);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t small = ~(((w[j] & 0x7F7F7F7Fu) + 0x75757575u) | w[j]) & 0x80808080u;  // bytes < 0x0B
+      const uint32_t n4 = (small * 0x00204081u) >> 28;  // bits 7, 15, 23, 31 -> 0..3
+      const int word = 4 * q + j;                       // 0..31
+      nib[word >> 3] |= n4 << (4 * (word & 7));
+    }
+  }
+  m0 = nib[0] | ((uint64_t)nib[1] << 32);
+  m1 = nib[2] | ((uint64_t)nib[3] << 32);
+}
+
+// Pass A function of the thread's span at block-relative offset rel (positions + 1).
+__device__ inline LFn tsv_span_fn(const uint8_t* span, uint32_t rel) {
+  uint64_t mm[2];
+  tsv_events(span, mm[0], mm[1]);
+  uint32_t s0 = 0, s1 = 1, c0 = 0, c1 = 0, l0 = 0, l1 = 0, ln = 0;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    uint64_t x = mm[h];
+    while (x) {
+      const uint32_t bit = (uint32_t)__builtin_ctzll(x);
+      x &= x - 1;
+      const uint32_t o = 64 * h + bit, c = span[o], p1 = rel + o + 1;
+      if (c == 0x0Au) {
+        if (s0) ++c0, l0 = p1, s0 = 0;
+        if (s1) ++c1, l1 = p1, s1 = 0;
+      } else if (c == 0x09u) {
+        if (!s0) l0 = p1, s0 = 1;
+        if (!s1) l1 = p1, s1 = 1;
+      } else if (c == 0) {
+        ln = p1;
+      }
+    }
+  }
+  return LFn{s0 | (s1 << 1) | (c0 << 2) | (c1 << 17), l0 | (l1 << 16), ln};
+}
+
+// Pass A: each block's function.
+__global__ __launch_bounds__(kTThreads) void tsv_fn_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                           GFn* __restrict__ blk_fn) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
+  typedef hipcub::BlockScan<LFn, kTThreads> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  tsv_stage(f, size, blockIdx.x, lds);
+  const uint32_t rel = kTBytes * threadIdx.x;
+  const LFn t = (uint64_t)blockIdx.x * kTChunk + rel < size ? tsv_span_fn(lds + 16 + rel, rel) : lfn_id();
+  LFn inc;
+  Scan(tmp).InclusiveScan(t, inc, LCompose());
+  if (threadIdx.x == kTThreads - 1) blk_fn[blockIdx.x] = gfn_of(inc, (uint64_t)blockIdx.x * kTChunk);
+}
+
+// Record count: the whole file's function from the start state, plus the record a
+// value getline ends at EOF.
+__global__ void tsv_count_kernel(const GFn* __restrict__ excl, const GFn* __restrict__ blk_fn, uint64_t nblk,
+                                 uint64_t* __restrict__ out) {
+  const TState e = gapply(GCompose()(excl[nblk - 1], blk_fn[nblk - 1]), TState{0, 0, 0, 0});
+  out[0] = e.r + e.m;
+}
+
+// Key hash from the staged block (key [off, off + len) inside it; chunk 0 may read up to
+// 15 bytes below, into the pad or the block's own earlier bytes, masked): h1 / h2 of the
+// key + NUL as hash_cstr computes them.
+__device__ inline void hash_cstr_lds(const uint8_t* lds_key, uint64_t len, const SpadTable& sp, uint64_t& h1,
+                                     uint64_t& h2) {
+  uint64_t raw = sp.v[0];
+  if (len) {
+    const uint32_t k = (uint32_t)((len + 15) / 16), p = (uint32_t)(16 * k - len);
+    const uint8_t* c0 = lds_key - p;
+    uint4 c = ld16(c0);
+    const uint32_t m0 = p >= 4 ? 0u : ~0u << (8 * p), m1 = p >= 8 ? 0u : p <= 4 ? ~0u : ~0u << (8 * (p - 4));
+    const uint32_t m2 = p >= 12 ? 0u : p <= 8 ? ~0u : ~0u << (8 * (p - 8)), m3 = p <= 12 ? ~0u : ~0u << (8 * (p - 12));
+    c.x &= m0, c.y &= m1, c.z &= m2, c.w &= m3;
+    uint32_t lo = (uint32_t)sp.v[p], hi = (uint32_t)(sp.v[p] >> 32);
+    for (uint32_t q = 1; q < k; ++q) {
+      const uint4 nx = ld16(c0 + 16 * q);
+      fnv_chunk16(lo, hi, c);
+      c = nx;
+    }
+    fnv_chunk16(lo, hi, c);
+    raw = ((uint64_t)hi << 32) | lo;
+  }
+  h1 = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
+  h2 = len ? raw : h1;
+}
+
+// Pass B: the walk.  Fields are written (and keys hashed) only for records below
+// min(count, cap), so a key cut off by EOF writes nothing.
+template <bool HASH>
+__global__ __launch_bounds__(kTThreads) void tsv_walk_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                             const GFn* __restrict__ excl,
+                                                             const uint64_t* __restrict__ count, uint64_t cap,
+                                                             k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
+                                                             uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
+  typedef hipcub::BlockScan<LFn, kTThreads> Scan;
+  __shared__ typename Scan::TempStorage tmp;
+  __shared__ uint64_t kl_off[HASH ? kTKeys : 1], kl_rec[HASH ? kTKeys : 1];
+  __shared__ uint32_t kl_len[HASH ? kTKeys : 1], kl_n;
+  if (HASH && threadIdx.x == 0) kl_n = 0;
+  tsv_stage(f, size, blockIdx.x, lds);  // (its barrier also publishes kl_n = 0)
+  const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
+  const uint32_t rel = kTBytes * threadIdx.x;
+  const uint8_t* span = lds + 16 + rel;
+  const bool live = base + rel < size;
+  const LFn t = live ? tsv_span_fn(span, rel) : lfn_id();
+  LFn pre;
+  Scan(tmp).ExclusiveScan(t, pre, lfn_id(), LCompose());
+  TState s = gapply(gfn_of(pre, base), gapply(excl[blockIdx.x], TState{0, 0, 0, 0}));
+  const uint64_t lim = min(count[0], cap);
+  bool nulf = s.ln > s.fs;  // a NUL already cut the current field
+  auto key_end = [&](uint64_t e) {
+    if (s.r >= lim) return;
+    recs[s.r].key_off = s.fs;
+    recs[s.r].key_len = e - s.fs;
+    if constexpr (HASH) {
+      uint32_t slot = kTKeys;
+      if (s.fs >= base) slot = __hip_atomic_fetch_add(&kl_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (slot < kTKeys) {
+        kl_off[slot] = s.fs;
+        kl_len[slot] = (uint32_t)(e - s.fs);
+        kl_rec[slot] = s.r;
+      } else {  // starts before the block, or the list is full: hash it here from HBM
+        uint64_t a, c;
+        hash_cstr(f, s.fs, e - s.fs, sp, a, c);
+        h1[s.r] = a;
+        if (h2) h2[s.r] = c;
+      }
+    }
+  };
+  auto val_end = [&](uint64_t e) {
+    if (s.r >= lim) return;
+    recs[s.r].val_off = s.fs;
+    recs[s.r].val_len = e - s.fs;
+  };
+  if (live) {
+    uint64_t mm[2];
+    tsv_events(span, mm[0], mm[1]);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint64_t x = mm[h];
+      while (x) {
+        const uint32_t bit = (uint32_t)__builtin_ctzll(x);
+        x &= x - 1;
+        const uint32_t o = 64 * h + bit, c = span[o];
+        const uint64_t pos = base + rel + o;
+        if (c == 0x0Au) {
+          if (s.m) {  // the value getline's newline: the record ends
+            if (!nulf) val_end(pos);
+            s.m = 0;
+            ++s.r;
+            s.fs = pos + 1;
+            nulf = false;
+          }
+        } else if (c == 0x09u) {
+          if (!s.m) {  // the key getline's TAB
+            if (!nulf) key_end(pos);
+            s.m = 1;
+            s.fs = pos + 1;
+            nulf = false;
+          }
+        } else if (c == 0 && !nulf) {  // the field's first NUL: its C string ends here
+          if (s.m) val_end(pos);
+          else key_end(pos);
+          nulf = true;
+        }
+      }
+    }
+    // the thread holding the last byte: a value read to EOF
+    if (base + rel + kTBytes >= size && s.m && !nulf) val_end(size);
+  }
+  if constexpr (HASH) {
+    __syncthreads();
+    const uint32_t nk = min(kl_n, (uint32_t)kTKeys);
+    for (uint32_t i = threadIdx.x; i < nk; i += kTThreads) {
+      uint64_t a, c;
+      hash_cstr_lds(lds + 16 + (kl_off[i] - base), kl_len[i], sp, a, c);
+      h1[kl_rec[i]] = a;
+      if (h2) h2[kl_rec[i]] = c;
+    }
+  }
+}
+
 }  // namespace
 
 __global__ void scan_summary_kernel(const uint8_t* __restrict__ f, uint64_t size, const uint64_t* __restrict__ bbase,
-                                    const uint64_t* __restrict__ rbase, const uint32_t* __restrict__ bst,
-                                    const uint32_t* __restrict__ bin, uint64_t nblk, uint64_t* __restrict__ out) {
+                                    uint64_t nblk, uint64_t* __restrict__ out) {
   out[0] = bbase[nblk];
-  out[1] = rbase[nblk];
-  out[2] = f[size - 1];
-  out[3] = SpanOp()(bin[nblk - 1], bst[nblk - 1]);
+  out[1] = f[size - 1];
 }
 
 // Scratch for the per-call temporaries: a library-private stream-ordered pool per device
@@ -453,6 +623,52 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
   return pools[dev] ? hipMallocFromPoolAsync(p, bytes, pools[dev], stream) : hipMallocAsync(p, bytes, stream);
 }
 
+// TSV: pass A, the scan of block functions, the count, pass B (when recs), one read-back.
+static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
+                      hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
+  const uint64_t nblk = (size + kTChunk - 1) / kTChunk;
+  GFn *fn = nullptr, *excl = nullptr;
+  uint64_t* dcount = nullptr;
+  void* tmp = nullptr;
+  size_t tmp_bytes = 0;
+  hipError_t e = nblk > 0x7FFFFFFFull ? hipErrorInvalidValue : hipSuccess;
+  auto tr = [&](hipError_t x) {
+    if (e == hipSuccess) e = x;
+  };
+  tr(scratch_alloc((void**)&fn, nblk * sizeof(GFn), stream));
+  tr(scratch_alloc((void**)&excl, nblk * sizeof(GFn), stream));
+  tr(scratch_alloc((void**)&dcount, 8, stream));
+  if (e == hipSuccess) {
+    tsv_fn_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn);
+    e = hipGetLastError();
+  }
+  tr(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp_bytes, fn, excl, GCompose(), gfn_id(), nblk, stream));
+  tr(scratch_alloc(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
+  tr(hipcub::DeviceScan::ExclusiveScan(tmp, tmp_bytes, fn, excl, GCompose(), gfn_id(), nblk, stream));
+  if (e == hipSuccess) {
+    tsv_count_kernel<<<1, 1, 0, stream>>>(excl, fn, nblk, dcount);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess && recs && cap) {
+    if (h1)
+      tsv_walk_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, dcount, cap, recs,
+                                                                      make_spad(seed), h1, h2);
+    else
+      tsv_walk_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, dcount, cap, recs,
+                                                                       SpadTable{}, nullptr, nullptr);
+    e = hipGetLastError();
+  }
+  uint64_t n = 0;
+  tr(hipMemcpyAsync(&n, dcount, 8, hipMemcpyDeviceToHost, stream));
+  tr(hipStreamSynchronize(stream));
+  for (void* p : {(void*)fn, (void*)excl, (void*)dcount, tmp})
+    if (p) (void)hipFreeAsync(p, stream);
+  *herr = e;
+  if (e != hipSuccess) return K2H_AMD_EHIP;
+  *count = n;
+  return (recs && n > cap) ? K2H_AMD_EINVAL : K2H_AMD_OK;
+}
+
 // Returns K2H_AMD_* codes (the HIP error, if any, in *herr).
 int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_import_rec* recs, uint64_t cap,
                        uint64_t* count, hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2,
@@ -464,9 +680,9 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   if (size == 0) return format == K2H_AMD_IMPORT_TSV ? K2H_AMD_OK : K2H_AMD_EINVAL;
   const uint64_t nblk = (size + kChunk - 1) / kChunk;
   if (nblk > 0x7FFFFFFFull) return K2H_AMD_EINVAL;
-  uint64_t* bcnt = nullptr;
-  uint64_t *bbase = nullptr, *nl = nullptr, *rl = nullptr, *brec2 = nullptr, *brec = nullptr, *rbase = nullptr;
-  LineInfo* info = nullptr;
+  if (format == K2H_AMD_IMPORT_TSV) return launch_tsv(f, size, recs, cap, count, stream, herr, h1, h2, seed);
+  // mdbm
+  uint64_t *bcnt = nullptr, *bbase = nullptr, *nl = nullptr, *lnul = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   uint32_t *bst = nullptr, *bin = nullptr;
@@ -477,84 +693,43 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   do {             \
     if (e == hipSuccess) e = (x); \
   } while (0)
-  const bool tsv = format == K2H_AMD_IMPORT_TSV;
-  if (nblk) {
-    K2H_TRY(scratch_alloc((void**)&bcnt, nblk * 8, stream));
-    K2H_TRY(scratch_alloc((void**)&bbase, (nblk + 1) * 8, stream));
-    K2H_TRY(scratch_alloc((void**)&bst, nblk * 4, stream));
-    K2H_TRY(scratch_alloc((void**)&bin, nblk * 4, stream));
-    K2H_TRY(scratch_alloc((void**)&brec2, nblk * 8, stream));
-    K2H_TRY(scratch_alloc((void**)&brec, nblk * 8, stream));
-    K2H_TRY(scratch_alloc((void**)&rbase, (nblk + 1) * 8, stream));
-    if (e == hipSuccess) {
-      span_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt, bst, brec2);
-      e = hipGetLastError();
-    }
-    K2H_TRY(hipMemsetAsync(bbase, 0, 8, stream));
-    K2H_TRY(hipMemsetAsync(rbase, 0, 8, stream));
-    size_t t1 = 0, t2 = 0;
-    K2H_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t1, bcnt, bbase + 1, nblk, stream));
-    K2H_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, t2, bst, bin, SpanOp(), 0u, nblk, stream));
-    tmp_bytes = t1 > t2 ? t1 : t2;
-    K2H_TRY(scratch_alloc(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
-    K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, bcnt, bbase + 1, nblk, stream));
-    K2H_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, t2, bst, bin, SpanOp(), 0u, nblk, stream));
-    if (e == hipSuccess) {
-      block_recs_kernel<<<blocks_for(nblk), kThreads, 0, stream>>>(brec2, bin, nblk, brec);
-      e = hipGetLastError();
-    }
-    K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, brec, rbase + 1, nblk, stream));  // same shape as bcnt
-    // one read-back: newline count, newline record ends, last byte, final span state
-    uint64_t sum[4] = {0, 0, '\n', 0};
-    uint64_t* dsum = nullptr;
-    K2H_TRY(scratch_alloc((void**)&dsum, sizeof sum, stream));
-    if (e == hipSuccess) {
-      scan_summary_kernel<<<1, 1, 0, stream>>>(f, size, bbase, rbase, bst, bin, nblk, dsum);
-      e = hipGetLastError();
-    }
-    K2H_TRY(hipMemcpyAsync(sum, dsum, sizeof sum, hipMemcpyDeviceToHost, stream));
-    K2H_TRY(hipStreamSynchronize(stream));
-    if (dsum) (void)hipFreeAsync(dsum, stream);
-    nnl = sum[0];
-    const uint64_t nrec_nl = sum[1];
-    const uint8_t last = (uint8_t)sum[2];
-    const uint32_t st_final = (uint32_t)sum[3];
-    // lines: one per newline, plus the bytes after the last newline if any
-    nlines = nnl + (last != '\n' ? 1 : 0);
-    // TSV records: newlines ending a TAB line, plus an open last line holding a TAB
-    if (tsv) nrec = nrec_nl + ((last != '\n' && (st_final & kTab)) ? 1 : 0);
-    // TSV needs pass 2 only to fill records; mdbm always (its header check reads nl)
-    const bool pass2 = !tsv || (recs && nrec && nrec <= cap);
-    if (pass2) {
-      K2H_TRY(scratch_alloc((void**)&nl, (nnl ? nnl : 1) * 8, stream));
-      K2H_TRY(scratch_alloc((void**)&info, (nlines ? nlines : 1) * sizeof(LineInfo), stream));
-      if (tsv) K2H_TRY(scratch_alloc((void**)&rl, nrec * 8, stream));
-      if (nlines) K2H_TRY(hipMemsetAsync(info, 0xFF, nlines * sizeof(LineInfo), stream));  // kNone
-      if (e == hipSuccess) {
-        span_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, bin, rbase, nl, info, rl);
-        e = hipGetLastError();
-      }
-    }
+  K2H_TRY(scratch_alloc((void**)&bcnt, nblk * 8, stream));
+  K2H_TRY(scratch_alloc((void**)&bbase, (nblk + 1) * 8, stream));
+  K2H_TRY(scratch_alloc((void**)&bst, nblk * 4, stream));
+  K2H_TRY(scratch_alloc((void**)&bin, nblk * 4, stream));
+  if (e == hipSuccess) {
+    span_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt, bst);
+    e = hipGetLastError();
   }
-  uint64_t* nul_from = nullptr;
-  void* tmp2 = nullptr;
-  if (e == hipSuccess && tsv) {
-    if (recs && nrec && nrec <= cap) {
-      hipcub::CountingInputIterator<uint64_t> idx(0);
-      hipcub::TransformInputIterator<uint64_t, NulLineRev, hipcub::CountingInputIterator<uint64_t>> nul_rev(
-          idx, NulLineRev{info, nlines});
-      size_t t3 = 0;
-      K2H_TRY(scratch_alloc((void**)&nul_from, nlines * 8, stream));
-      K2H_TRY(hipcub::DeviceScan::InclusiveScan(nullptr, t3, nul_rev, nul_from, MinOp(), nlines, stream));
-      K2H_TRY(scratch_alloc(&tmp2, t3 ? t3 : 1, stream));
-      K2H_TRY(hipcub::DeviceScan::InclusiveScan(tmp2, t3, nul_rev, nul_from, MinOp(), nlines, stream));
-      if (e == hipSuccess) {
-        tsv_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, nul_from, nlines, rl, nrec,
-                                                                      recs, f, make_spad(seed), h1, h2);
-        e = hipGetLastError();
-      }
-    }
-  } else if (e == hipSuccess && format == K2H_AMD_IMPORT_MDBM) {
+  K2H_TRY(hipMemsetAsync(bbase, 0, 8, stream));
+  size_t t1 = 0, t2 = 0;
+  K2H_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t1, bcnt, bbase + 1, nblk, stream));
+  K2H_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, t2, bst, bin, SpanOp(), 0u, nblk, stream));
+  tmp_bytes = t1 > t2 ? t1 : t2;
+  K2H_TRY(scratch_alloc(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
+  K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, bcnt, bbase + 1, nblk, stream));
+  K2H_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, t2, bst, bin, SpanOp(), 0u, nblk, stream));
+  // one read-back: newline count, last byte
+  uint64_t sum[2] = {0, '\n'};
+  uint64_t* dsum = nullptr;
+  K2H_TRY(scratch_alloc((void**)&dsum, sizeof sum, stream));
+  if (e == hipSuccess) {
+    scan_summary_kernel<<<1, 1, 0, stream>>>(f, size, bbase, nblk, dsum);
+    e = hipGetLastError();
+  }
+  K2H_TRY(hipMemcpyAsync(sum, dsum, sizeof sum, hipMemcpyDeviceToHost, stream));
+  K2H_TRY(hipStreamSynchronize(stream));
+  if (dsum) (void)hipFreeAsync(dsum, stream);
+  nnl = sum[0];
+  nlines = nnl + ((uint8_t)sum[1] != '\n' ? 1 : 0);  // the bytes after the last newline, if any
+  K2H_TRY(scratch_alloc((void**)&nl, (nnl ? nnl : 1) * 8, stream));
+  K2H_TRY(scratch_alloc((void**)&lnul, (nlines ? nlines : 1) * 8, stream));
+  if (nlines) K2H_TRY(hipMemsetAsync(lnul, 0xFF, nlines * 8, stream));  // kNone
+  if (e == hipSuccess) {
+    span_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, bin, nl, lnul);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) {
     // header: five getline calls; the fifth must extract exactly "HEADER=END"
     static const char kEnd[] = "HEADER=END";
     uint64_t hb = 0, he = 0, body = 0;
@@ -577,7 +752,7 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
     if (e == hipSuccess && ok) {
       nrec = nlines > 5 ? (nlines - 5 + 1) / 2 : 0;
       if (recs && nrec && nrec <= cap) {
-        mdbm_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, info, nlines, nrec, body,
+        mdbm_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, lnul, nlines, nrec, body,
                                                                           recs, f, make_spad(seed), h1, h2);
         e = hipGetLastError();
       }
@@ -585,8 +760,7 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   }
   K2H_TRY(hipStreamSynchronize(stream));
 #undef K2H_TRY
-  for (void* p : {(void*)bcnt, (void*)bbase, (void*)bst, (void*)bin, (void*)brec2, (void*)brec, (void*)rbase, (void*)nl,
-                  (void*)rl, (void*)info, tmp, (void*)nul_from, tmp2})
+  for (void* p : {(void*)bcnt, (void*)bbase, (void*)bst, (void*)bin, (void*)nl, (void*)lnul, tmp})
     if (p) (void)hipFreeAsync(p, stream);
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;
