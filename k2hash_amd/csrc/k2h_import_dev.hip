@@ -439,18 +439,26 @@ __device__ inline LFn tsv_span_fn(const uint8_t* span, uint32_t rel) {
   return LFn{s0 | (s1 << 1) | (c0 << 2) | (c1 << 17), l0 | (l1 << 16), ln};
 }
 
-// Pass A: each block's function.
+// Pass A: each block's function, and each thread's prefix within its block (three
+// coalesced words per thread, so pass B needs neither the span functions nor the scan).
 __global__ __launch_bounds__(kTThreads) void tsv_fn_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                           GFn* __restrict__ blk_fn) {
+                                                           GFn* __restrict__ blk_fn, uint32_t* __restrict__ pa,
+                                                           uint32_t* __restrict__ pb, uint32_t* __restrict__ pc) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
   typedef hipcub::BlockScan<LFn, kTThreads> Scan;
   __shared__ typename Scan::TempStorage tmp;
   tsv_stage(f, size, blockIdx.x, lds);
   const uint32_t rel = kTBytes * threadIdx.x;
   const LFn t = (uint64_t)blockIdx.x * kTChunk + rel < size ? tsv_span_fn(lds + 16 + rel, rel) : lfn_id();
-  LFn inc;
-  Scan(tmp).InclusiveScan(t, inc, LCompose());
-  if (threadIdx.x == kTThreads - 1) blk_fn[blockIdx.x] = gfn_of(inc, (uint64_t)blockIdx.x * kTChunk);
+  LFn pre, agg;
+  Scan(tmp).ExclusiveScan(t, pre, lfn_id(), LCompose(), agg);
+  const uint64_t i = (uint64_t)blockIdx.x * kTThreads + threadIdx.x;
+  if (pa) {
+    pa[i] = pre.a;
+    pb[i] = pre.b;
+    pc[i] = pre.c;
+  }
+  if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(agg, (uint64_t)blockIdx.x * kTChunk);
 }
 
 // Record count: the whole file's function from the start state, plus the record a
@@ -492,12 +500,13 @@ __device__ inline void hash_cstr_lds(const uint8_t* lds_key, uint64_t len, const
 template <bool HASH>
 __global__ __launch_bounds__(kTThreads) void tsv_walk_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                              const GFn* __restrict__ excl,
+                                                             const uint32_t* __restrict__ pa,
+                                                             const uint32_t* __restrict__ pb,
+                                                             const uint32_t* __restrict__ pc,
                                                              const uint64_t* __restrict__ count, uint64_t cap,
                                                              k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
                                                              uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
-  typedef hipcub::BlockScan<LFn, kTThreads> Scan;
-  __shared__ typename Scan::TempStorage tmp;
   __shared__ uint64_t kl_off[HASH ? kTKeys : 1], kl_rec[HASH ? kTKeys : 1];
   __shared__ uint32_t kl_len[HASH ? kTKeys : 1], kl_n;
   if (HASH && threadIdx.x == 0) kl_n = 0;
@@ -506,9 +515,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_walk_kernel(const uint8_t* __re
   const uint32_t rel = kTBytes * threadIdx.x;
   const uint8_t* span = lds + 16 + rel;
   const bool live = base + rel < size;
-  const LFn t = live ? tsv_span_fn(span, rel) : lfn_id();
-  LFn pre;
-  Scan(tmp).ExclusiveScan(t, pre, lfn_id(), LCompose());
+  const uint64_t ti = (uint64_t)blockIdx.x * kTThreads + threadIdx.x;
+  const LFn pre{pa[ti], pb[ti], pc[ti]};
   TState s = gapply(gfn_of(pre, base), gapply(excl[blockIdx.x], TState{0, 0, 0, 0}));
   const uint64_t lim = min(count[0], cap);
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
@@ -623,12 +631,24 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
   return pools[dev] ? hipMallocFromPoolAsync(p, bytes, pools[dev], stream) : hipMallocAsync(p, bytes, stream);
 }
 
+// The TSV per-thread prefixes (12 B per 128 B of file): a grow-only buffer per device,
+// held across calls while it stays within kScratchKeep (larger ones are freed at the end
+// of the call), under a per-device lock for the duration of the call -- a pool
+// allocation of this size cost ~0.5 ms per call.
+struct PrefixCache {
+  std::mutex mu;
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+PrefixCache g_prefix[64];
+
 // TSV: pass A, the scan of block functions, the count, pass B (when recs), one read-back.
 static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
                       hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
   const uint64_t nblk = (size + kTChunk - 1) / kTChunk;
   GFn *fn = nullptr, *excl = nullptr;
   uint64_t* dcount = nullptr;
+  uint32_t* pre = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   hipError_t e = nblk > 0x7FFFFFFFull ? hipErrorInvalidValue : hipSuccess;
@@ -638,8 +658,31 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   tr(scratch_alloc((void**)&fn, nblk * sizeof(GFn), stream));
   tr(scratch_alloc((void**)&excl, nblk * sizeof(GFn), stream));
   tr(scratch_alloc((void**)&dcount, 8, stream));
+  const bool walk = recs && cap;
+  int dev = 0;
+  tr(hipGetDevice(&dev));
+  if (e == hipSuccess && (dev < 0 || dev >= 64)) e = hipErrorInvalidDevice;
+  PrefixCache& pc_ = g_prefix[e == hipSuccess ? dev : 0];
+  std::unique_lock<std::mutex> lk(pc_.mu, std::defer_lock);
+  const size_t pre_bytes = walk ? nblk * kTThreads * 12 : 0;
+  if (e == hipSuccess && walk) {
+    lk.lock();
+    if (pc_.bytes < pre_bytes) {
+      if (pc_.p) tr(hipFree(pc_.p));
+      pc_.p = nullptr;
+      pc_.bytes = 0;
+      tr(hipMalloc(&pc_.p, pre_bytes));
+      if (e == hipSuccess) pc_.bytes = pre_bytes;
+    }
+    pre = (uint32_t*)pc_.p;
+  }
+  uint32_t *pa = pre, *pb = pre + (walk ? nblk * kTThreads : 0), *pc = pb + (walk ? nblk * kTThreads : 0);
   if (e == hipSuccess) {
-    tsv_fn_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn);
+    // (count only: no prefixes)
+    if (walk)
+      tsv_fn_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, pa, pb, pc);
+    else
+      tsv_fn_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, nullptr, nullptr, nullptr);
     e = hipGetLastError();
   }
   tr(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp_bytes, fn, excl, GCompose(), gfn_id(), nblk, stream));
@@ -651,10 +694,10 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   }
   if (e == hipSuccess && recs && cap) {
     if (h1)
-      tsv_walk_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, dcount, cap, recs,
+      tsv_walk_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, pa, pb, pc, dcount, cap, recs,
                                                                       make_spad(seed), h1, h2);
     else
-      tsv_walk_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, dcount, cap, recs,
+      tsv_walk_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, pa, pb, pc, dcount, cap, recs,
                                                                        SpadTable{}, nullptr, nullptr);
     e = hipGetLastError();
   }
@@ -663,6 +706,11 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   tr(hipStreamSynchronize(stream));
   for (void* p : {(void*)fn, (void*)excl, (void*)dcount, tmp})
     if (p) (void)hipFreeAsync(p, stream);
+  if (lk.owns_lock() && pc_.bytes > kScratchKeep) {  // the stream is synchronised: no kernel still reads it
+    (void)hipFree(pc_.p);
+    pc_.p = nullptr;
+    pc_.bytes = 0;
+  }
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;
   *count = n;
