@@ -413,28 +413,38 @@ __device__ inline void tsv_events(const uint8_t* span, uint64_t& m0, uint64_t& m
   m1 = nib[2] | ((uint64_t)nib[3] << 32);
 }
 
+// Consume the lowest event of the 128-bit mask pair: its offset, or 128 when none is left.
+__device__ inline uint32_t next_event(uint64_t& m0, uint64_t& m1) {
+  const bool lo = m0 != 0;
+  const uint64_t x = lo ? m0 : m1;
+  const uint32_t b = x ? (uint32_t)__builtin_ctzll(x) + (lo ? 0u : 64u) : 128u;
+  const uint64_t xn = x & (x - 1);
+  m0 = lo ? xn : 0;
+  m1 = lo ? m1 : xn;
+  return b;
+}
+
 // Pass A function of the thread's span at block-relative offset rel (positions + 1).
 __device__ inline LFn tsv_span_fn(const uint8_t* span, uint32_t rel) {
   uint64_t mm[2];
   tsv_events(span, mm[0], mm[1]);
   uint32_t s0 = 0, s1 = 1, c0 = 0, c1 = 0, l0 = 0, l1 = 0, ln = 0;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    uint64_t x = mm[h];
-    while (x) {
-      const uint32_t bit = (uint32_t)__builtin_ctzll(x);
-      x &= x - 1;
-      const uint32_t o = 64 * h + bit, c = span[o], p1 = rel + o + 1;
-      if (c == 0x0Au) {
-        if (s0) ++c0, l0 = p1, s0 = 0;
-        if (s1) ++c1, l1 = p1, s1 = 0;
-      } else if (c == 0x09u) {
-        if (!s0) l0 = p1, s0 = 1;
-        if (!s1) l1 = p1, s1 = 1;
-      } else if (c == 0) {
-        ln = p1;
-      }
+  // one loop over all events, the next event's byte read from LDS while this one is handled
+  uint32_t o = next_event(mm[0], mm[1]), c = span[o & 127u];
+  while (o < 128) {
+    const uint32_t on = next_event(mm[0], mm[1]), cn = span[on & 127u];
+    const uint32_t p1 = rel + o + 1;
+    if (c == 0x0Au) {
+      if (s0) ++c0, l0 = p1, s0 = 0;
+      if (s1) ++c1, l1 = p1, s1 = 0;
+    } else if (c == 0x09u) {
+      if (!s0) l0 = p1, s0 = 1;
+      if (!s1) l1 = p1, s1 = 1;
+    } else if (c == 0) {
+      ln = p1;
     }
+    o = on;
+    c = cn;
   }
   return LFn{s0 | (s1 << 1) | (c0 << 2) | (c1 << 17), l0 | (l1 << 16), ln};
 }
@@ -547,13 +557,10 @@ __global__ __launch_bounds__(kTThreads) void tsv_walk_kernel(const uint8_t* __re
   if (live) {
     uint64_t mm[2];
     tsv_events(span, mm[0], mm[1]);
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      uint64_t x = mm[h];
-      while (x) {
-        const uint32_t bit = (uint32_t)__builtin_ctzll(x);
-        x &= x - 1;
-        const uint32_t o = 64 * h + bit, c = span[o];
+    uint32_t o = next_event(mm[0], mm[1]), c = span[o & 127u];
+    while (o < 128) {
+      const uint32_t on = next_event(mm[0], mm[1]), cn = span[on & 127u];
+      {
         const uint64_t pos = base + rel + o;
         if (c == 0x0Au) {
           if (s.m) {  // the value getline's newline: the record ends
@@ -576,6 +583,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_walk_kernel(const uint8_t* __re
           nulf = true;
         }
       }
+      o = on;
+      c = cn;
     }
     // the thread holding the last byte: a value read to EOF
     if (base + rel + kTBytes >= size && s.m && !nulf) val_end(size);
