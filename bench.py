@@ -16,7 +16,7 @@ Every rank's shard is checked against the reference's digests
 (tests/golden/digests.json, fixed32_1G chunks) outside the timed region.
 
 At N = 1 the line also carries secondary results (configs 3, 4 and 5, config 2 with the fused
-bucket index, RALLEDATA blobs and the
+bucket index, RALLEDATA blobs, the k2himport TSV scan + prehash of a file in HBM, and the
 host-memory path) and a CPU baseline: the reference's own hash path (oracle/_ref),
 timed on this host's cores.
 
@@ -342,7 +342,7 @@ def chunks_of(length: int) -> int:
 
 
 # --------------------------------------------------------------------------------------
-# Secondary results at N = 1 (configs 3, 4, 5 and the host-memory path)
+# Secondary results at N = 1 (configs 3, 4, 5, SURVEY 8f rows 1-3 and the host-memory path)
 # --------------------------------------------------------------------------------------
 def secondary_csr(dev, steps, warm_ms, verify):
     import torch
@@ -451,6 +451,66 @@ def secondary_ralledata(dev, steps, warm_ms, verify):
             digest_dev(boff, 0) == g["blob_off"]
         res["verify"] = {"ok": ok, "against": "tests/golden/ralledata_digest.json"}
     del ko, vo, kd, vd, blob, boff
+    torch.cuda.empty_cache()
+    return res
+
+
+IMPORT_N, IMPORT_KEY_LENS, IMPORT_VAL_LENS, IMPORT_BYTE_OFF = 1 << 23, (8, 64), (0, 200), 1 << 34
+
+
+def import_workload(dev):
+    """bench's k2himport TSV workload, built on the device: 2^23 records "key TAB value
+    NEWLINE" (key lengths 8-64, value lengths 0-200, printable bytes) -- the file
+    tests/golden/make_import_digest.py builds on the host from the same generators."""
+    import torch
+
+    from k2hash_amd import batch
+
+    n = IMPORT_N
+    kl = batch.synth_offsets(n, dev, *IMPORT_KEY_LENS, seed=batch.SEED_LENS + 11).diff()
+    vl = batch.synth_offsets(n, dev, *IMPORT_VAL_LENS, seed=batch.SEED_LENS + 13).diff()
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(kl + vl + 2, dim=0, out=off[1:])
+    data = batch.synth_bytes(int(off[-1].item()), dev, byte_off=IMPORT_BYTE_OFF)
+    data.remainder_(95).add_(32)
+    data[off[:-1] + kl] = 9
+    data[off[1:] - 1] = 10
+    return data
+
+
+def secondary_import(dev, steps, warm_ms, verify):
+    """k2himport's TSV loop (tests/k2himport.cc:81-86) over a file resident
+    in HBM -- records (key / value offsets and C-string lengths) and every key's h1 / h2 as
+    K2HShm::Set(const char*) hashes it, from one call (k2h_amd_import_scan_prehash_device,
+    which synchronises its stream: the step time is the call's wall time).  Checked against
+    tests/golden/import_digest.json (the tool's own getline loop + the reference hash)."""
+    import torch
+
+    from k2hash_amd import archive
+
+    data = import_workload(dev)
+    n, size = IMPORT_N, data.numel()
+    out = {}
+
+    def step(i):
+        out["r"] = archive.import_scan_prehash_device(data)
+
+    wall, kern, _ = timed(step, steps, 2, warm_ms)
+    algo = size + 32 * n + 16 * n  # the file once, the records, the two hashes
+    model = sum(chunks_of(L) for L in range(IMPORT_KEY_LENS[0], IMPORT_KEY_LENS[1] + 1)) / \
+        (IMPORT_KEY_LENS[1] - IMPORT_KEY_LENS[0] + 1) * FNV_OPS_PER_CHUNK * n / 64
+    res = {"workload": f"{n} TSV records (keys 8-64 B, values 0-200 B, {size} B file in HBM) -> records + h1/h2",
+           "records": n, "file_bytes": size, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
+           "value": n * steps / wall, "unit": "records/s", "file_gb_per_s": size * steps / wall / 1e9,
+           "roofline": roofline("import", algo, wall / steps, model)}
+    if verify:
+        recs, h1, h2 = out["r"]
+        g = json.loads((ROOT / "tests" / "golden" / "import_digest.json").read_text())
+        cols = {"key_off": recs[:, 0], "key_len": recs[:, 1], "val_off": recs[:, 2], "val_len": recs[:, 3],
+                "h1": h1, "h2": h2}
+        ok = g["records"] == recs.shape[0] == n and all(digest_dev(v.contiguous(), 0) == g[k] for k, v in cols.items())
+        res["verify"] = {"ok": bool(ok), "against": "tests/golden/import_digest.json"}
+    del data, out
     torch.cuda.empty_cache()
     return res
 
@@ -722,6 +782,7 @@ def main():
                 "fixed32_1g": secondary_fixed("fixed32_1g", dev, 10, 60.0, vf, "fixed32_1G"),
                 "fixed32_index": secondary_index(dev, 20, 60.0, vf),
                 "ralledata": secondary_ralledata(dev, 20, 60.0, vf),
+                "import": secondary_import(dev, 10, 60.0, vf),
                 "host": secondary_host(dev),
             }
         if not args.no_cpu_baseline:

@@ -14,6 +14,9 @@
 // before each getline, C-string key / value bytes in hex, the two hashes) or an error.
 //
 //   gen_import tsv|mdbm <file>
+//   gen_import tsv-digest <file>   the TSV loop's records and hashes as order-sensitive
+//                                  digests {xor, sum, sum of v * (2i + 1)} per field (the
+//                                  bench's 8M-record workload, tests/golden/make_import_digest.py)
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -28,10 +31,61 @@ static void hex(const char* p, size_t n) {
   for (size_t i = 0; i < n; ++i) printf("%02x", (unsigned)(unsigned char)p[i]);
 }
 
+struct Digest {  // oracle_digest (oracle/fnv_oracle.c), accumulated one value at a time
+  uint64_t x = 0, s = 0, w = 0;
+  void add(uint64_t v, uint64_t i) {
+    x ^= v;
+    s += v;
+    w += v * (2 * i + 1);
+  }
+  void print(const char* name) const {
+    printf("\"%s\": [\"%016llx\", \"%016llx\", \"%016llx\"]", name, (unsigned long long)x, (unsigned long long)s,
+           (unsigned long long)w);
+  }
+};
+
+static int tsv_digest(std::ifstream& is) {
+  Digest d[6];
+  uint64_t n = 0;
+  std::string key, value;
+  for (;;) {  // the loop of tests/k2himport.cc:81-86
+    long long koff = (long long)is.tellg();
+    if (!std::getline(is, key, '\t')) break;
+    if (is.eof()) break;
+    long long voff = (long long)is.tellg();
+    std::getline(is, value);
+    const char* kc = key.c_str();
+    const size_t kl = strlen(kc), vl = strlen(value.c_str());
+    d[0].add((uint64_t)koff, n);
+    d[1].add(kl, n);
+    d[2].add((uint64_t)voff, n);
+    d[3].add(vl, n);
+    d[4].add(k2h_hash(kc, kl + 1), n);
+    d[5].add(k2h_second_hash(kc, kl + 1), n);
+    ++n;
+  }
+  static const char* names[6] = {"key_off", "key_len", "val_off", "val_len", "h1", "h2"};
+  printf("{\"format\": \"tsv\", \"records\": %llu", (unsigned long long)n);
+  for (int k = 0; k < 6; ++k) {
+    printf(", ");
+    d[k].print(names[k]);
+  }
+  printf("}\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc != 3) {
-    fprintf(stderr, "usage: gen_import tsv|mdbm <file>\n");
+    fprintf(stderr, "usage: gen_import tsv|mdbm|tsv-digest <file>\n");
     return 2;
+  }
+  if (strcmp(argv[1], "tsv-digest") == 0) {
+    std::ifstream is(argv[2], std::ios::binary);
+    if (!is) {
+      fprintf(stderr, "cannot open %s\n", argv[2]);
+      return 2;
+    }
+    return tsv_digest(is);
   }
   const bool tsv = strcmp(argv[1], "tsv") == 0;
   std::ifstream is(argv[2], std::ios::binary);

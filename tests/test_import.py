@@ -232,3 +232,26 @@ def test_device_scan_long_multiline_key(cuda, nul_line):
     for shift in (0, 3):
         _, _, got = _dev_scan_np(cuda, data, "tsv", shift)
         assert np.array_equal(got, archive.import_scan(data, "tsv")), (nul_line, shift)
+
+
+@pytest.mark.gpu
+def test_bench_import_workload_digest(cuda):
+    """bench.py's import secondary: the 8M-record TSV built on the device, scanned and
+    prehashed in one call, equals k2himport's own getline loop + the reference hash over
+    the same file (tests/golden/import_digest.json, tests/golden/make_import_digest.py)."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, str(GOLDEN.parents[1]))
+    import bench
+
+    data = bench.import_workload(cuda)
+    recs, h1, h2 = archive.import_scan_prehash_device(data)
+    torch.cuda.synchronize()
+    g = json.loads((GOLDEN / "import_digest.json").read_text())
+    assert g["bytes"] == data.numel() and g["records"] == recs.shape[0] == bench.IMPORT_N
+    cols = {"key_off": recs[:, 0], "key_len": recs[:, 1], "val_off": recs[:, 2], "val_len": recs[:, 3], "h1": h1,
+            "h2": h2}
+    for k, v in cols.items():
+        assert bench.digest_dev(v.contiguous(), 0) == g[k], k
