@@ -328,7 +328,9 @@ enum {
   kModeStaged = 0, kModeDirect = 1, kModeRing = 2, kModeStagedPairs = 3, kModeStagedSingle = 4, kModeStagedProf = 5,
   kModeLean256 = 6, kModeLean512x8 = 7, kModeLean512x4 = 8, kModeLeanAlignProbe = 9, kModeLeanRing = 10,
   kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13, kModeLean2Group = 14,
-  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23
+  kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
+  kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
+  kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -1201,6 +1203,493 @@ __global__ __launch_bounds__(NW * 64) void fnv_csr_pair_kernel(const uint8_t* __
 }
 
 // ---------------------------------------------------------------------------
+// CSR double-buffered tiles (round 2).  One persistent 512-thread block per CU walks
+// the 512-key tiles blockIdx, blockIdx + grid, ...  with two LDS tile slots (stage,
+// tile-relative offsets, sorted order), and its waves split by role:
+//   waves 0-3  hash tile j from slot j&1 (pair walk, as fnv_csr_lean2_kernel WALK 3);
+//   wave 4     prepares tile j+1 in the other slot: offsets -> LDS, counting sort by
+//              chunk count (one wave, so no block barrier inside the sort), tile info;
+//   waves 5-7  DMA tile j+1's byte span into the other slot's stage.
+// One s_barrier per tile hands a prepared slot to the hash waves and the slot they
+// just finished to the feeders.  The feeders prefetch tile j+2's offsets into registers
+// during tile j+1's preparation, so the offset load, the sort and the span DMA -- 45 %
+// of a lean2 tile's life, during which its waves issued no hash work -- all run under
+// the hash of the previous tile.  Each role is its own loop: the hash waves' code never
+// follows a global_load_lds, so hipcc puts no vmcnt drain in front of their LDS reads.
+// Tiles whose span exceeds the stage go to the ring list, as in lean2.
+// PROBE (lab timing probes, wrong hashes): 1 = hash waves do not hash (feeder-bound
+// time), 2 = feeders prepare the first two tiles only (hash-bound time).
+// ---------------------------------------------------------------------------
+template <bool H2, bool EPI = false, int PROBE = 0>
+__global__ __launch_bounds__(512) void fnv_csr_dbuf_kernel(const uint8_t* __restrict__ bytes,
+                                                           const uint64_t* __restrict__ offsets, uint64_t n,
+                                                           SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                           uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
+                                                           uint32_t* __restrict__ over_count, BucketParams bp = {}) {
+  constexpr uint32_t TK = 512, NB = 128, NDMA = 3;
+  constexpr uint32_t kStage = 72 * 1024u;
+  constexpr uint32_t kSlot = 16 + kStage + 1024u;  // + the overhang of the span's last 1 KiB DMA piece
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[2 * kSlot];
+  __shared__ uint32_t s_rel[2 * (TK + 1)];
+  __shared__ uint16_t s_order[2 * TK];
+  __shared__ uint32_t s_info[4];  // per slot: key count (0 = not staged here), stage lead delta
+  __shared__ uint32_t s_hist[NB];
+  __shared__ uint64_t s_spad[16];
+  __shared__ uint4 s_mask[16];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t ntiles = (n + TK - 1) / TK;
+  const uint64_t first = blockIdx.x, stride = gridDim.x;
+  const uint32_t J = first < ntiles ? (uint32_t)((ntiles - first + stride - 1) / stride) : 0u;
+  if (tid < 16) {
+    s_spad[tid] = spad_tab.v[tid];
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
+      int32_t sh = 8 * ((int32_t)tid - 4 * i);
+      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
+    }
+    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __syncthreads();
+  auto tile_cnt = [n](uint64_t t0) -> uint32_t { return (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK); };
+  auto rfl64 = [](uint64_t v) -> uint64_t {
+    // (readfirstlane returns int: each half goes through uint32_t, or the low one sign-extends)
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  };
+  const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
+
+  if (wave < 4) {  // ---- hash waves ----
+    for (uint32_t j = 0; j < J; ++j) {
+      lds_barrier();
+      const uint32_t b = j & 1u;
+      const uint32_t cnt = __builtin_amdgcn_readfirstlane(s_info[2 * b]);
+      if (cnt == 0) continue;
+      if constexpr (PROBE == 1) continue;
+      const uint32_t delta = __builtin_amdgcn_readfirstlane(s_info[2 * b + 1]);
+      const uint64_t t0 = (first + (uint64_t)j * stride) * TK;
+      const uint16_t* ord = s_order + b * TK;
+      const uint32_t* rel = s_rel + b * (TK + 1);
+      const uint8_t* key0 = s_stage + b * kSlot + 16 + delta;
+      const uint32_t i = tid;
+      const bool has_a = i < (cnt + 1u) / 2u, has_b = i < cnt / 2u;
+      const uint32_t ka = ord[has_a ? i : 0u], kbi = ord[has_b ? cnt - 1u - i : 0u];
+      const uint32_t ra = rel[ka], rae = rel[ka + 1], rb = rel[kbi], rbe = rel[kbi + 1];
+      const uint32_t la = has_a ? rae - ra : 0u, lb = has_b ? rbe - rb : 0u;
+      const uint32_t kA = (la + 15u) >> 4, kB = (lb + 15u) >> 4;
+      const uint32_t pA = (0u - la) & 15u, pB = (0u - lb) & 15u;
+      const uint8_t* cpA = key0 + (int32_t)(rae - 16u * kA);
+      const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
+      const bool only_b = kA == 0;
+      uint64_t hw0, hw1;
+      pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
+                hw0, hw1);
+      const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
+      if (has_a) {
+        h1[t0 + ka] = hA;
+        if constexpr (H2) h2[t0 + ka] = second_from_first(hA, la, key0 + rae);
+        if constexpr (EPI) bucket_emit<false>(bp, t0 + ka, hA);
+      }
+      if (has_b) {
+        h1[t0 + kbi] = hB;
+        if constexpr (H2) h2[t0 + kbi] = second_from_first(hB, lb, key0 + rbe);
+        if constexpr (EPI) bucket_emit<false>(bp, t0 + kbi, hB);
+      }
+    }
+    return;
+  }
+
+  if (wave == 4) {  // ---- sort wave: offsets, length classes, order, tile info ----
+    uint32_t pa[9];
+    uint64_t pz = 0, pe = 0;
+    // (per-lane vector loads through an index the compiler cannot see is zero: no scalar
+    // loads, whose out-of-order return would turn every LDS wait into lgkmcnt(0))
+    auto fetch = [&](uint64_t tile) {
+      const uint64_t t0 = tile * TK;
+      const uint32_t cnt = tile_cnt(t0);
+      uint32_t zero = 0;
+      asm volatile("" : "+v"(zero));
+#pragma unroll
+      for (uint32_t q = 0; q < 9; ++q) {
+        const uint32_t k = lane + 64u * q;
+        pa[q] = off32[2 * (t0 + (k < cnt ? k : cnt))];
+      }
+      pz = offsets[t0 + zero];
+      pe = offsets[t0 + cnt + zero];
+    };
+    if (J) fetch(first);
+    for (uint32_t j = 0; j < J; ++j) {
+      const uint32_t b = j & 1u;
+      const uint64_t tile = first + (uint64_t)j * stride, t0 = tile * TK;
+      const uint32_t cnt = tile_cnt(t0);
+      const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
+      if (PROBE == 2 && j >= 2) {
+        lds_barrier();
+        continue;
+      }
+      uint32_t cur[9];
+#pragma unroll
+      for (uint32_t q = 0; q < 9; ++q) cur[q] = pa[q] - (uint32_t)o0;
+      if (j + 1 < J) fetch(tile + stride);
+      const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
+      const uint32_t delta = (uint32_t)(kb & 15u);
+      const uint64_t span = oN - o0 + delta;
+      if (span > kStage) {
+        if (lane == 0) {
+          over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
+          s_info[2 * b] = 0;
+        }
+      } else {
+        uint32_t* rel = s_rel + b * (TK + 1);
+        uint16_t* ord = s_order + b * TK;
+#pragma unroll
+        for (uint32_t q = 0; q < 9; ++q) {
+          const uint32_t k = lane + 64u * q;
+          if (k <= cnt) rel[k] = cur[q];
+        }
+        s_hist[lane] = 0;
+        s_hist[lane + 64] = 0;
+        uint32_t bins[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+          const uint32_t k = lane + 64u * q;
+          // key k's end offset: the next lane's value (lane 63: lane 0 of the next row);
+          // taken with every lane active
+          const uint32_t nx = (uint32_t)__shfl_down((int)cur[q], 1, 64);
+          const uint32_t n0 = __builtin_amdgcn_readfirstlane(cur[q + 1]);
+          bins[q] = len_bin128_32((lane == 63 ? n0 : nx) - cur[q]);
+          if (k < cnt) lds_add(&s_hist[bins[q]], 1u);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t v0 = s_hist[2 * lane], v1 = s_hist[2 * lane + 1], sum = v0 + v1;
+        uint32_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          uint32_t y = __shfl_up(incl, d, 64);
+          if (lane >= (uint32_t)d) incl += y;
+        }
+        s_hist[2 * lane] = incl - sum;
+        s_hist[2 * lane + 1] = incl - sum + v0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+          const uint32_t k = lane + 64u * q;
+          if (k < cnt) ord[lds_add_rtn(&s_hist[bins[q]], 1u)] = (uint16_t)k;
+        }
+        if (lane == 0) {
+          s_info[2 * b] = cnt;
+          s_info[2 * b + 1] = delta;
+        }
+      }
+      lds_barrier();  // slot b prepared (LDS writes complete); the hash waves start on it
+    }
+    return;
+  }
+
+  // ---- DMA waves: tile j's byte span into slot j&1's stage ----
+  {
+    const uint32_t dw = wave - 5u;
+    uint64_t pz = 0, pe = 0;
+    auto fetch = [&](uint64_t tile) {
+      const uint64_t t0 = tile * TK;
+      const uint32_t cnt = tile_cnt(t0);
+      uint32_t zero = 0;
+      asm volatile("" : "+v"(zero));
+      pz = offsets[t0 + zero];
+      pe = offsets[t0 + cnt + zero];
+    };
+    if (J) fetch(first);
+    for (uint32_t j = 0; j < J; ++j) {
+      const uint32_t b = j & 1u;
+      const uint64_t tile = first + (uint64_t)j * stride;
+      const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
+      if (PROBE == 2 && j >= 2) {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+        continue;
+      }
+      if (j + 1 < J) fetch(tile + stride);
+      const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
+      const uint64_t span_lo = kb & ~15ull;
+      const uint64_t span = oN - o0 + (kb & 15u);
+      if (span <= kStage && oN > o0) {
+        // 1 KiB pieces, 16 B per lane; lanes past the span re-read its last 16 B into
+        // stage bytes nobody reads
+        const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
+        const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
+        const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
+        uint8_t* dst = s_stage + b * kSlot + 16;
+        uint32_t off = 1024u * dw + 16u * lane;
+        for (uint32_t c = dw; c < npieces; c += NDMA, off += 1024u * NDMA) {
+          const uint32_t o = off < lastp ? off : lastp;
+          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
+                                           (__attribute__((address_space(3))) void*)(dst + 1024u * c), 16, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // slot b's bytes have landed
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CSR queue tiles (round 2).  One persistent 768-thread block per CU, two LDS tile slots
+// (stage, tile-relative offsets, length-sorted order) and waves split by role:
+//   waves 0-7   hash: each claims 64-key groups of the tile in its current slot (longest
+//               first) from an LDS counter, one key per lane, and moves on to the next
+//               tile when the slot has no group left -- two hash waves per SIMD at all
+//               times, the FNV chain of one wave alone being latency-bound (a single
+//               wave per SIMD ran the same tiles at ~290 ns per chunk step instead of
+//               ~165, fnv_csr_dbuf_kernel);
+//   wave 8      sort: tile offsets -> LDS, counting sort by chunk count, tile info;
+//   waves 9-11  DMA the tile's byte span into the slot's stage.
+// A slot is refilled once all eight hash waves have left the tile it held; the feeders
+// prefetch the next tile's offsets into registers, so offset loads, sort and DMA run
+// under the hash of the previous tile and no block-wide barrier is taken per tile.
+// Control words per slot (cumulative counters, never reset, except the claim counter,
+// which only the sort wave touches while no hash wave is in the slot):
+//   [0] ready: tile index + 1 of the tile the slot holds, [1] claims, [2] hash waves
+//   left, [3] feeder waves done, [4] key count (0 = not staged: ring list), [5] delta.
+// Tiles whose span exceeds the stage go to the ring list, as in lean2.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t lds_u32addr(const uint32_t* p) {
+  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)p;
+}
+// A control word read that waits for its value (polling / after a flag: no reordering).
+__device__ __forceinline__ uint32_t lds_poll(const uint32_t* p) {
+  uint32_t v;
+  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_u32addr(p)) : "memory");
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t target) {
+  while (lds_poll(p) < target) __builtin_amdgcn_s_sleep(1);
+}
+
+// PROBE (lab timing probes, wrong hashes): 1 = hash waves claim groups without hashing,
+// 2 = feeders stage the first two tiles only (later tiles re-hash stale slots);
+// 3 (correct hashes) = feeder waves at raised issue priority.
+template <bool H2, bool EPI = false, int PROBE = 0>
+__global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __restrict__ bytes,
+                                                            const uint64_t* __restrict__ offsets, uint64_t n,
+                                                            SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                            uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
+                                                            uint32_t* __restrict__ over_count, BucketParams bp = {}) {
+  constexpr uint32_t TK = 512, NB = 128, NH = 8, NDMA = 3, NF = 1 + NDMA;
+  constexpr uint32_t kStage = 72 * 1024u;
+  constexpr uint32_t kSlot = 16 + kStage + 1024u;  // + the overhang of the span's last 1 KiB DMA piece
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[2 * kSlot];
+  __shared__ uint32_t s_rel[2 * (TK + 1)];
+  __shared__ uint16_t s_order[2 * TK];
+  __shared__ uint32_t s_ctl[16];
+  __shared__ uint32_t s_hist[NB];
+  __shared__ uint64_t s_spad[16];
+  __shared__ uint4 s_mask[16];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t ntiles = (n + TK - 1) / TK;
+  const uint64_t first = blockIdx.x, stride = gridDim.x;
+  const uint32_t J = first < ntiles ? (uint32_t)((ntiles - first + stride - 1) / stride) : 0u;
+  if (tid < 16) {
+    s_spad[tid] = spad_tab.v[tid];
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
+      int32_t sh = 8 * ((int32_t)tid - 4 * i);
+      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
+    }
+    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+    s_ctl[tid] = 0;
+  }
+  __syncthreads();
+  auto tile_cnt = [n](uint64_t t0) -> uint32_t { return (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK); };
+  auto rfl64 = [](uint64_t v) -> uint64_t {
+    // (readfirstlane returns int: each half goes through uint32_t, or the low one sign-extends)
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+  };
+  // a feeder wave's part of tile j is in LDS: count it; the last of the NF publishes the slot
+  auto feeder_done = [&](uint32_t j) {
+    uint32_t* ctl = s_ctl + 8u * (j & 1u);
+    uint32_t old = 0;
+    if (lane == 0) old = lds_add_rtn(&ctl[3], 1u);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if (old == NF * ((j >> 1) + 1u) - 1u && lane == 0)
+      asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_u32addr(&ctl[0])), "v"(j + 1u) : "memory");
+  };
+  const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
+
+  if (wave < NH) {  // ---- hash waves ----
+    for (uint32_t j = 0; j < J; ++j) {
+      const uint32_t b = j & 1u;
+      uint32_t* ctl = s_ctl + 8u * b;
+      lds_wait_ge(&ctl[0], j + 1u);
+      const uint32_t cnt = lds_poll(&ctl[4]);
+      const uint32_t delta = lds_poll(&ctl[5]);
+      const uint32_t ngroups = (cnt + 63u) >> 6;
+      const uint64_t t0 = (first + (uint64_t)j * stride) * TK;
+      const uint16_t* ord = s_order + b * TK;
+      const uint32_t* rel = s_rel + b * (TK + 1);
+      const uint8_t* key0 = s_stage + b * kSlot + 16 + delta;
+      for (;;) {
+        uint32_t c = 0;
+        if (lane == 0) c = lds_add_rtn(&ctl[1], 1u);
+        c = __builtin_amdgcn_readfirstlane(c);
+        if (c >= ngroups) break;
+        if constexpr (PROBE == 1) continue;
+        const uint32_t idx = 64u * (ngroups - 1u - c) + lane;  // longest groups first
+        const bool valid = idx < cnt;
+        const uint32_t k = ord[valid ? idx : cnt - 1u];
+        uint64_t r1, r2;
+        lds_hash32<false>(valid, rel[k], rel[k + 1], key0, s_spad, s_mask, r1, r2);
+        if (valid) {
+          h1[t0 + k] = r1;
+          if constexpr (H2) h2[t0 + k] = r2;
+          if constexpr (EPI) bucket_emit<false>(bp, t0 + k, r1);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the slot has returned
+      if (lane == 0) lds_add(&ctl[2], 1u);                 // this wave has left the slot
+    }
+    return;
+  }
+
+  // the feeders issue ahead of the hash waves sharing their SIMD (PROBE 3)
+  if constexpr (PROBE == 3) __builtin_amdgcn_s_setprio(3);
+  if (wave == NH) {  // ---- sort wave: offsets, length classes, order, tile info ----
+    uint32_t pa[9];
+    uint64_t pz = 0, pe = 0;
+    // (per-lane vector loads through an index the compiler cannot see is zero: no scalar
+    // loads, whose out-of-order return would turn every LDS wait into lgkmcnt(0))
+    auto fetch = [&](uint64_t tile) {
+      const uint64_t t0 = tile * TK;
+      const uint32_t cnt = tile_cnt(t0);
+      uint32_t zero = 0;
+      asm volatile("" : "+v"(zero));
+#pragma unroll
+      for (uint32_t q = 0; q < 9; ++q) {
+        const uint32_t k = lane + 64u * q;
+        pa[q] = off32[2 * (t0 + (k < cnt ? k : cnt) + zero)];
+      }
+      pz = offsets[t0 + zero];
+      pe = offsets[t0 + cnt + zero];
+    };
+    if (J) fetch(first);
+    for (uint32_t j = 0; j < J; ++j) {
+      const uint32_t b = j & 1u;
+      uint32_t* ctl = s_ctl + 8u * b;
+      const uint64_t tile = first + (uint64_t)j * stride, t0 = tile * TK;
+      const uint32_t cnt = tile_cnt(t0);
+      const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
+      uint32_t cur[9];
+#pragma unroll
+      for (uint32_t q = 0; q < 9; ++q) cur[q] = pa[q] - (uint32_t)o0;
+      if (j + 1 < J) fetch(tile + stride);
+      const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
+      const uint32_t delta = (uint32_t)(kb & 15u);
+      const uint64_t span = oN - o0 + delta;
+      lds_wait_ge(&ctl[2], NH * (j >> 1));  // every hash wave has left the slot's previous tile
+      if (PROBE == 2 && j >= 2) {
+        if (lane == 0) ctl[1] = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        feeder_done(j);
+        continue;
+      }
+      uint32_t* rel = s_rel + b * (TK + 1);
+      uint16_t* ord = s_order + b * TK;
+      const bool staged = span <= kStage;
+      if (!staged) {
+        if (lane == 0) over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
+      } else {
+#pragma unroll
+        for (uint32_t q = 0; q < 9; ++q) {
+          const uint32_t k = lane + 64u * q;
+          if (k <= cnt) rel[k] = cur[q];
+        }
+        s_hist[lane] = 0;
+        s_hist[lane + 64] = 0;
+        uint32_t bins[8];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+          const uint32_t k = lane + 64u * q;
+          // key k's end offset: the next lane's value (lane 63: lane 0 of the next row);
+          // taken with every lane active
+          const uint32_t nx = (uint32_t)__shfl_down((int)cur[q], 1, 64);
+          const uint32_t n0 = __builtin_amdgcn_readfirstlane(cur[q + 1]);
+          bins[q] = len_bin128_32((lane == 63 ? n0 : nx) - cur[q]);
+          if (k < cnt) lds_add(&s_hist[bins[q]], 1u);
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint32_t v0 = s_hist[2 * lane], v1 = s_hist[2 * lane + 1], sum = v0 + v1;
+        uint32_t incl = sum;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          uint32_t y = __shfl_up(incl, d, 64);
+          if (lane >= (uint32_t)d) incl += y;
+        }
+        s_hist[2 * lane] = incl - sum;
+        s_hist[2 * lane + 1] = incl - sum + v0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q) {
+          const uint32_t k = lane + 64u * q;
+          if (k < cnt) ord[lds_add_rtn(&s_hist[bins[q]], 1u)] = (uint16_t)k;
+        }
+      }
+      if (lane == 0) {
+        ctl[1] = 0;  // claims (no hash wave is in the slot)
+        ctl[4] = staged ? cnt : 0u;
+        ctl[5] = delta;
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      feeder_done(j);
+    }
+    return;
+  }
+
+  // ---- DMA waves: tile j's byte span into slot j&1's stage ----
+  {
+    const uint32_t dw = wave - (NH + 1u);
+    uint64_t pz = 0, pe = 0;
+    auto fetch = [&](uint64_t tile) {
+      const uint64_t t0 = tile * TK;
+      const uint32_t cnt = tile_cnt(t0);
+      uint32_t zero = 0;
+      asm volatile("" : "+v"(zero));
+      pz = offsets[t0 + zero];
+      pe = offsets[t0 + cnt + zero];
+    };
+    if (J) fetch(first);
+    for (uint32_t j = 0; j < J; ++j) {
+      const uint32_t b = j & 1u;
+      const uint64_t tile = first + (uint64_t)j * stride;
+      const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
+      if (j + 1 < J) fetch(tile + stride);
+      const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
+      const uint64_t span_lo = kb & ~15ull;
+      const uint64_t span = oN - o0 + (kb & 15u);
+      lds_wait_ge(&s_ctl[8u * b + 2u], NH * (j >> 1));  // the slot's previous tile is consumed
+      if (span <= kStage && oN > o0 && !(PROBE == 2 && j >= 2)) {
+        // 1 KiB pieces, 16 B per lane; lanes past the span re-read its last 16 B into
+        // stage bytes nobody reads
+        const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
+        const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
+        const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
+        uint8_t* dst = s_stage + b * kSlot + 16;
+        uint32_t off = 1024u * dw + 16u * lane;
+        for (uint32_t c = dw; c < npieces; c += NDMA, off += 1024u * NDMA) {
+          const uint32_t o = off < lastp ? off : lastp;
+          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
+                                           (__attribute__((address_space(3))) void*)(dst + 1024u * c), 16, 0, 0);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces have landed
+      feeder_done(j);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Fixed-length keys other than the 32-byte fast path (e.g. BASELINE config 5,
 // 4 KiB): one lane per key, the same chunk walker, uniform trip count.
 // ---------------------------------------------------------------------------
@@ -1431,10 +1920,54 @@ static hipError_t launch_pair(const uint8_t* b, const uint64_t* offsets, uint64_
   return e != hipSuccess ? e : f;
 }
 
+// Double-buffered tile kernel (one persistent block per CU) + the ring pass over its
+// oversize-tile list.
+template <int PROBE = 0, bool QUEUE = false>
+[[maybe_unused]] static hipError_t launch_dbuf(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
+                              uint64_t* h2, const BucketParams* bp, hipStream_t stream) {
+  constexpr uint64_t TK = 512;
+  const uint64_t ntiles = (n + TK - 1) / TK;
+  if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  uint32_t* scratch = nullptr;  // [0] = count, [1..] = tile list
+  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (ntiles + 1), stream);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(scratch, 0, 4, stream);
+  const BucketParams none{};
+  const BucketParams& p = bp ? *bp : none;
+  const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
+#define K2H_DBUF(H2, EPI)                                                                                        \
+  {                                                                                                            \
+    constexpr auto k = QUEUE ? fnv_csr_queue_kernel<H2, EPI, PROBE> : fnv_csr_dbuf_kernel<H2, EPI, PROBE>;               \
+    constexpr int nt = QUEUE ? 768 : 512;                                                                      \
+    const unsigned g = resident_grid<k>(nt, (unsigned)ntiles);                                                 \
+    k<<<g, nt, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, scratch + 1, scratch, p);                 \
+    fnv_csr_ring_list_kernel<H2, EPI, (int)TK><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, \
+                                                                       scratch + 1, scratch, p);               \
+  }
+  if (e == hipSuccess) {
+    if (bp) {
+      if (h2) K2H_DBUF(true, true) else K2H_DBUF(false, true)
+    } else {
+      if (h2) K2H_DBUF(true, false) else K2H_DBUF(false, false)
+    }
+    e = hipGetLastError();
+  }
+#undef K2H_DBUF
+  hipError_t f = hipFreeAsync(scratch, stream);
+  return e != hipSuccess ? e : f;
+}
+
 #if K2H_AMD_LAB
 static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
   SpadTable t = make_spad(seed);
+  if (mode == kModeDbufProbeNoHash) return launch_dbuf<1>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModeDbufProbeNoFeed) return launch_dbuf<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModeQueueProbeNoHash) return launch_dbuf<1, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModeQueuePrio) return launch_dbuf<3, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModeQueue) return launch_dbuf<0, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModeDbuf) return launch_dbuf((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair2) return launch_pair<2, 36, false>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair2P) return launch_pair<2, 36, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModePair4P) return launch_pair<4, 72, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);

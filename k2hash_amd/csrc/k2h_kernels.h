@@ -100,6 +100,14 @@ enum {
   kVariantRallePieces2 = 79,      // gather form, two output pieces per loop trip
   kVariantRalleStageAll = 80,     // gather form, staged loads on all four waves
   kVariantCsrPair4Z = 69,         // csr pair tiles (512 keys), the mad64 zero half kept in v50 across the walk
+  kVariantCsrDbuf = 81,           // csr: double-buffered 512-key tiles, one persistent block per CU, hash / sort /
+                                  // DMA waves split by role
+  kVariantCsrDbufProbeNoHash = 82,  // timing probes (WRONG hashes): dbuf without hashing / without feeding
+  kVariantCsrDbufProbeNoFeed = 83,
+  kVariantCsrQueue = 84,          // csr: queue tiles (8 hash waves claim 64-key groups, sort / DMA feeder waves)
+  kVariantCsrQueueProbeNoHash = 85,  // timing probes (WRONG hashes): queue tiles without hashing / without feeding
+  kVariantCsrQueueProbeNoFeed = 86,
+  kVariantCsrQueuePrio = 87,      // csr queue tiles, feeder waves at raised issue priority
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };

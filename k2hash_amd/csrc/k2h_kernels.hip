@@ -826,6 +826,13 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrPair4W2 ? 21
                          : variant == kVariantCsrPair4Z ? 22
                          : variant == kVariantCsrClock ? 23
+                         : variant == kVariantCsrDbuf ? 24
+                         : variant == kVariantCsrQueue ? 27
+                         : variant == kVariantCsrQueuePrio ? 30
+                         : variant == kVariantCsrQueueProbeNoHash ? 28
+                         : variant == kVariantCsrQueueProbeNoFeed ? 29
+                         : variant == kVariantCsrDbufProbeNoHash ? 25
+                         : variant == kVariantCsrDbufProbeNoFeed ? 26
                                                         : 11,
                          stream, epi ? bp : nullptr);
 }
