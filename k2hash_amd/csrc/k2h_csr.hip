@@ -330,7 +330,8 @@ enum {
   kModeLean2Ring = 11, kModeLean2Pin = 12, kModeLean2Step = 13, kModeLean2Group = 14,
   kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
   kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
-  kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30
+  kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30,
+  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -863,8 +864,10 @@ __device__ __forceinline__ void pair_walk2(uint32_t k0, uint32_t p0, const uint8
 }
 
 // CLK (lab clock probe, H2 false): h2 receives per wave the shader-clock / 100 MHz stamps
-// at entry and after the hash (tools/clock_probe.py)
-template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false>
+// at entry and after the hash (tools/clock_probe.py).  PRIO (lab): the load / sort phase at
+// raised issue priority, back to normal for the hash walk, so a tile's setup is not queued
+// behind the other block's hash instructions on the same SIMD.
+template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0>
 __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
                                                             SpadTable spad_tab, uint64_t* __restrict__ h1,
@@ -885,6 +888,7 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
     clk0 = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const uint64_t t0 = (uint64_t)blockIdx.x * TK;
@@ -957,6 +961,7 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
   __syncthreads();                                   // ... and every other wave's
 
   const uint8_t* key0 = s_stage + 16 + delta;
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
   if constexpr (WALK == 3) {
     // Pair walk: lane i (0..255) takes sorted keys i and cnt-1-i, a short and a long one,
     // and hashes them back to back; sums of the pair lengths are nearly equal across a
@@ -1740,6 +1745,7 @@ __global__ __launch_bounds__(256) void fnv_fixed_long_kernel(const uint8_t* __re
 // ---------------------------------------------------------------------------
 // PROBE (timing probes only, wrong hashes): 1 = no DMA (hash whatever LDS holds),
 // 2 = no hashing (DMA + waits only).
+// PROBE 4 (lab, correct hashes): each round's DMA issued at raised issue priority.
 template <bool H2, int D, int RB, bool EPI = false, int PROBE = 0>
 __global__ __launch_bounds__(64) void fnv_fixed_lines_kernel(const uint8_t* __restrict__ base, uint64_t key_len,
                                                              uint64_t n, uint64_t seed, uint64_t* __restrict__ h1,
@@ -1772,10 +1778,12 @@ __global__ __launch_bounds__(64) void fnv_fixed_lines_kernel(const uint8_t* __re
     if constexpr (PROBE == 1) return;
     uint8_t* slot = ring + (q % D) * (64u * RB);
     const uint8_t* src = wbase + (uint64_t)RB * q;
+    if constexpr (PROBE == 4) __builtin_amdgcn_s_setprio(2);
 #pragma unroll
     for (uint32_t i = 0; i < NP; ++i)
       __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + voff[i]),
                                        (__attribute__((address_space(3))) void*)(slot + 1024u * i), 16, 0, 0);
+    if constexpr (PROBE == 4) __builtin_amdgcn_s_setprio(0);
   };
 
   uint64_t clk0 = 0, rt0 = 0;
@@ -1841,24 +1849,30 @@ SpadTable make_spad(uint64_t seed) {
 }
 
 // lean2 tile kernel (walk WALK) + the ring pass over its oversize-tile list.
+// Issue priority of lean2's load / sort phase (s_setprio; the hash walk runs at 0): a tile's
+// offset loads, DMA issue and length sort then do not queue behind the other block's hash
+// instructions on the same SIMD.  -2.8 % kernel time on config 3 in same-process A/B
+// (lab variants 88-90, priorities 1-3 equal; profiles/r02y_csr_dbuf_queue_ab.json).
+constexpr int kLean2Prio = 1;
+
 template <int WALK>
 static hipError_t launch_lean2(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
                                uint64_t* h2, uint32_t* scratch, unsigned g, unsigned gl, const BucketParams* bp,
                                hipStream_t stream) {
   if (bp) {
     if (h2) {
-      fnv_csr_lean2_kernel<true, true, WALK><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, *bp);
+      fnv_csr_lean2_kernel<true, true, WALK, false, kLean2Prio><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, *bp);
       fnv_csr_ring_list_kernel<true, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, *bp);
     } else {
-      fnv_csr_lean2_kernel<false, true, WALK><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, *bp);
+      fnv_csr_lean2_kernel<false, true, WALK, false, kLean2Prio><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, *bp);
       fnv_csr_ring_list_kernel<false, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, *bp);
     }
   } else {
     if (h2) {
-      fnv_csr_lean2_kernel<true, false, WALK><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<true, false, WALK, false, kLean2Prio><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
       fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
     } else {
-      fnv_csr_lean2_kernel<false, false, WALK><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<false, false, WALK, false, kLean2Prio><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
       fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
     }
   }
@@ -1957,6 +1971,30 @@ template <int PROBE = 0, bool QUEUE = false>
   return e != hipSuccess ? e : f;
 }
 
+// lean2 with its load / sort phase at issue priority PRIO (lab A/B)
+template <int PRIO>
+[[maybe_unused]] static hipError_t launch_lean2_prio(const uint8_t* bb, const uint64_t* offsets, uint64_t n,
+                                                     const SpadTable& t, uint64_t* h1, uint64_t* h2, hipStream_t stream) {
+  const unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
+  const unsigned gl = g < 512u ? g : 512u;
+  uint32_t* scratch = nullptr;
+  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (g + 1), stream);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(scratch, 0, 4, stream);
+  if (e == hipSuccess) {
+    if (h2) {
+      fnv_csr_lean2_kernel<true, false, 3, false, PRIO><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
+      fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
+    } else {
+      fnv_csr_lean2_kernel<false, false, 3, false, PRIO><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+    }
+    e = hipGetLastError();
+  }
+  hipError_t f = hipFreeAsync(scratch, stream);
+  return e != hipSuccess ? e : f;
+}
+
 #if K2H_AMD_LAB
 static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
@@ -1965,6 +2003,9 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModeDbufProbeNoFeed) return launch_dbuf<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeQueueProbeNoHash) return launch_dbuf<1, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
+  if (mode == kModeLean2Prio) return launch_lean2_prio<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2Prio3) return launch_lean2_prio<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2Prio1) return launch_lean2_prio<1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeQueuePrio) return launch_dbuf<3, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeQueue) return launch_dbuf<0, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeDbuf) return launch_dbuf((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
@@ -2126,7 +2167,7 @@ static hipError_t launch_fixed_long_lab(const void* keys, uint64_t key_len, uint
     // kLongLines2Pad / Pad2: 4 / 2 KiB of dynamic LDS on top of the 16 KiB ring, i.e. 8 or
     // 9 instead of 10 waves per CU (occupancy probes)
     const unsigned pad = mode == kLongLines2Pad ? 4096u : mode == kLongLines2Pad2 ? 2048u : 0u;
-    if ((mode >= kLongProbeCompute && mode <= kLongProbeMemHalf4) || mode == kLongProbeClock) {  // probes
+    if ((mode >= kLongProbeCompute && mode <= kLongProbeMemHalf4) || mode == kLongProbeClock || mode == kLongPrio) {  // probes
       if (mode == kLongProbeCompute)
         fnv_fixed_lines_kernel<false, 2, 128, false, 1><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
       else if (mode == kLongProbeMemory)
@@ -2139,6 +2180,8 @@ static hipError_t launch_fixed_long_lab(const void* keys, uint64_t key_len, uint
         fnv_fixed_lines_kernel<false, 2, 256, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
       else if (mode == kLongProbeMemHalf4)
         fnv_fixed_lines_kernel<false, 4, 64, false, 2><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      else if (mode == kLongPrio)
+        fnv_fixed_lines_kernel<false, 2, 128, false, 4><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
       else if (mode == kLongProbeClock && h2)
         fnv_fixed_lines_kernel<true, 2, 128, false, 3><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, h2);
       return hipGetLastError();

@@ -108,6 +108,11 @@ enum {
   kVariantCsrQueueProbeNoHash = 85,  // timing probes (WRONG hashes): queue tiles without hashing / without feeding
   kVariantCsrQueueProbeNoFeed = 86,
   kVariantCsrQueuePrio = 87,      // csr queue tiles, feeder waves at raised issue priority
+  kVariantCsrLean2Prio = 88,      // csr lean2 with its load / sort phase at raised issue priority (2; 89: 3, 90: 1)
+  kVariantCsrLean2Prio3 = 89,
+  kVariantCsrLean2Prio1 = 90,
+  kVariantFixed32Prio = 91,       // fixed32 default kernel with its loads issued at raised priority
+  kVariantLongPrio = 92,          // fixed long keys: line-DMA kernel, DMA issued at raised priority
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };
@@ -209,7 +214,8 @@ enum { kLongAuto = 0, kLongDirect = 1, kLongRing = 2, kLongLines2 = 3,
        kLongProbeCompute = 12, kLongProbeMemory = 13, kLongProbeMem3 = 14, kLongProbeMem4 = 15,
        kLongProbeMem256 = 16, kLongProbeMemHalf4 = 17,
        kLongHalf2 = 18,  // 2 half-line rounds (8 KiB per wave, 20 waves per CU)
-       kLongProbeClock = 19  // clock probe (h2 = per-wave shader-clock / 100 MHz stamps)
+       kLongProbeClock = 19,  // clock probe (h2 = per-wave shader-clock / 100 MHz stamps)
+       kLongPrio = 20         // the default line-DMA kernel with each round's DMA issued at raised priority (h1 only)
 #endif
 };
 bool fixed_lines_ok(const void* keys, uint64_t key_len);

@@ -254,7 +254,8 @@ __global__ __launch_bounds__(256) void fnv_fixed32_lds_kernel(const uint4* __res
 // fixed32, flat grid, KPT keys per thread: block b owns keys [b*256*KPT, (b+1)*256*KPT);
 // thread t hashes keys b*256*KPT + j*256 + t.  All 2*KPT loads are issued before the
 // first hash, so each wave keeps KPT*2 KiB in flight while it computes.
-template <bool H2, int KPT, int BS = 256, bool NT = false, bool EPI = false, bool CLK = false>
+// PRIO (lab): the loads issued at raised issue priority, the hash at 0.
+template <bool H2, int KPT, int BS = 256, bool NT = false, bool EPI = false, bool CLK = false, int PRIO = 0>
 __global__ __launch_bounds__(BS) void fnv_fixed32_kpt_kernel(const uint4* __restrict__ keys, uint64_t n,
                                                              uint64_t seed, uint64_t* __restrict__ h1,
                                                              uint64_t* __restrict__ h2, BucketParams bp = {}) {
@@ -265,6 +266,7 @@ __global__ __launch_bounds__(BS) void fnv_fixed32_kpt_kernel(const uint4* __rest
     clk0 = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const uint64_t base = (uint64_t)blockIdx.x * (BS * KPT) + threadIdx.x;
   uint4 a[KPT], b[KPT];
 #pragma unroll
@@ -280,6 +282,7 @@ __global__ __launch_bounds__(BS) void fnv_fixed32_kpt_kernel(const uint4* __rest
       }
     }
   }
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
     uint64_t i = base + BS * j;
@@ -554,6 +557,12 @@ static hipError_t launch_fixed_lab(const void* keys, uint64_t key_len, uint64_t 
         else fnv_fixed32_kpt_kernel<false, 2, 64, true><<<g, 64, 0, stream>>>(k, n, seed, h1, nullptr);
         break;
       }
+      case kVariantFixed32Prio: {
+        unsigned g = (unsigned)((n + 127) / 128);
+        if (h2) fnv_fixed32_kpt_kernel<true, 2, 64, true, false, false, 1><<<g, 64, 0, stream>>>(k, n, seed, h1, h2);
+        else fnv_fixed32_kpt_kernel<false, 2, 64, true, false, false, 1><<<g, 64, 0, stream>>>(k, n, seed, h1, nullptr);
+        break;
+      }
       case kVariantFixed32Pipe64: {
         const uint64_t nt = (n + 127) / 128;
         if (h2) fnv_fixed32_pipe_kernel<true, 64><<<pipe_grid<true, 64>(nt), 64, 0, stream>>>(k, n, seed, h1, h2);
@@ -670,6 +679,7 @@ static hipError_t launch_fixed_lab(const void* keys, uint64_t key_len, uint64_t 
                      : variant == kVariantLongHalf3  ? kLongHalf3
                      : variant == kVariantLongHalf2  ? kLongHalf2
                      : variant == kVariantLongClock  ? kLongProbeClock
+                     : variant == kVariantLongPrio   ? kLongPrio
                      : variant == kVariantLongHalf4  ? kLongHalf4
                      : variant == kVariantLongHalf6  ? kLongHalf6
                      : variant == kVariantLongHalf5  ? kLongHalf5
@@ -829,6 +839,9 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrDbuf ? 24
                          : variant == kVariantCsrQueue ? 27
                          : variant == kVariantCsrQueuePrio ? 30
+                         : variant == kVariantCsrLean2Prio ? 31
+                         : variant == kVariantCsrLean2Prio3 ? 32
+                         : variant == kVariantCsrLean2Prio1 ? 33
                          : variant == kVariantCsrQueueProbeNoHash ? 28
                          : variant == kVariantCsrQueueProbeNoFeed ? 29
                          : variant == kVariantCsrDbufProbeNoHash ? 25
