@@ -331,7 +331,7 @@ enum {
   kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
   kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
   kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30,
-  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33
+  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -867,7 +867,8 @@ __device__ __forceinline__ void pair_walk2(uint32_t k0, uint32_t p0, const uint8
 // at entry and after the hash (tools/clock_probe.py).  PRIO (lab): the load / sort phase at
 // raised issue priority, back to normal for the hash walk, so a tile's setup is not queued
 // behind the other block's hash instructions on the same SIMD.
-template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0>
+// SCAN1 (lab): the 128-class scan by wave 0 alone, two classes per lane (one barrier fewer).
+template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0, bool SCAN1 = false>
 __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
                                                             SpadTable spad_tab, uint64_t* __restrict__ h1,
@@ -940,17 +941,32 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
     }
   }
   lds_barrier();
-  uint32_t v = tid < NB ? s_hist[tid] : 0u, incl = v;
+  if constexpr (SCAN1) {
+    static_assert(NB == 128, "two classes per lane of wave 0");
+    if (wave == 0) {
+      const uint32_t v0 = s_hist[2 * lane], v1 = s_hist[2 * lane + 1], sum = v0 + v1;
+      uint32_t incl = sum;
 #pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    uint32_t y = __shfl_up(incl, d, 64);
-    if (lane >= (uint32_t)d) incl += y;
+      for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+      }
+      s_hist[2 * lane] = incl - sum;
+      s_hist[2 * lane + 1] = incl - sum + v0;
+    }
+  } else {
+    uint32_t v = tid < NB ? s_hist[tid] : 0u, incl = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      uint32_t y = __shfl_up(incl, d, 64);
+      if (lane >= (uint32_t)d) incl += y;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    lds_barrier();
+    uint32_t base = 0;
+    for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
+    if (tid < NB) s_hist[tid] = base + incl - v;
   }
-  if (lane == 63) s_wsum[wave] = incl;
-  lds_barrier();
-  uint32_t base = 0;
-  for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
-  if (tid < NB) s_hist[tid] = base + incl - v;
   lds_barrier();
 #pragma unroll
   for (uint32_t j = 0; j < KPT; ++j) {
@@ -1852,8 +1868,11 @@ SpadTable make_spad(uint64_t seed) {
 // Issue priority of lean2's load / sort phase (s_setprio; the hash walk runs at 0): a tile's
 // offset loads, DMA issue and length sort then do not queue behind the other block's hash
 // instructions on the same SIMD.  -2.8 % kernel time on config 3 in same-process A/B
-// (lab variants 88-90, priorities 1-3 equal; profiles/r02y_csr_dbuf_queue_ab.json).
+// (lab variants 88-90, priorities 1-3 equal; profiles/r02ba_csr_dbuf_queue_ab.json).
 constexpr int kLean2Prio = 1;
+// The 128-class scan by wave 0 alone (two classes per lane, one barrier fewer than the
+// four-wave scan): -0.6 % (lab variant 93 vs 90, profiles/r02ba_csr_dbuf_queue_ab.json).
+constexpr bool kLean2Scan1 = true;
 
 template <int WALK>
 static hipError_t launch_lean2(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
@@ -1861,18 +1880,18 @@ static hipError_t launch_lean2(const uint8_t* b, const uint64_t* offsets, uint64
                                hipStream_t stream) {
   if (bp) {
     if (h2) {
-      fnv_csr_lean2_kernel<true, true, WALK, false, kLean2Prio><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, *bp);
+      fnv_csr_lean2_kernel<true, true, WALK, false, kLean2Prio, kLean2Scan1><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, *bp);
       fnv_csr_ring_list_kernel<true, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch, *bp);
     } else {
-      fnv_csr_lean2_kernel<false, true, WALK, false, kLean2Prio><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, *bp);
+      fnv_csr_lean2_kernel<false, true, WALK, false, kLean2Prio, kLean2Scan1><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, *bp);
       fnv_csr_ring_list_kernel<false, true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch, *bp);
     }
   } else {
     if (h2) {
-      fnv_csr_lean2_kernel<true, false, WALK, false, kLean2Prio><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<true, false, WALK, false, kLean2Prio, kLean2Scan1><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
       fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, h2, scratch + 1, scratch);
     } else {
-      fnv_csr_lean2_kernel<false, false, WALK, false, kLean2Prio><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<false, false, WALK, false, kLean2Prio, kLean2Scan1><<<g, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
       fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, nullptr, scratch + 1, scratch);
     }
   }
@@ -1972,7 +1991,7 @@ template <int PROBE = 0, bool QUEUE = false>
 }
 
 // lean2 with its load / sort phase at issue priority PRIO (lab A/B)
-template <int PRIO>
+template <int PRIO, bool SCAN1 = false>
 [[maybe_unused]] static hipError_t launch_lean2_prio(const uint8_t* bb, const uint64_t* offsets, uint64_t n,
                                                      const SpadTable& t, uint64_t* h1, uint64_t* h2, hipStream_t stream) {
   const unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
@@ -1983,10 +2002,10 @@ template <int PRIO>
   e = hipMemsetAsync(scratch, 0, 4, stream);
   if (e == hipSuccess) {
     if (h2) {
-      fnv_csr_lean2_kernel<true, false, 3, false, PRIO><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<true, false, 3, false, PRIO, SCAN1><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
       fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
     } else {
-      fnv_csr_lean2_kernel<false, false, 3, false, PRIO><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<false, false, 3, false, PRIO, SCAN1><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
       fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
     }
     e = hipGetLastError();
@@ -2005,6 +2024,7 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeLean2Prio) return launch_lean2_prio<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio3) return launch_lean2_prio<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2Scan1) return launch_lean2_prio<1, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio1) return launch_lean2_prio<1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeQueuePrio) return launch_dbuf<3, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeQueue) return launch_dbuf<0, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);

@@ -113,6 +113,7 @@ enum {
   kVariantCsrLean2Prio1 = 90,
   kVariantFixed32Prio = 91,       // fixed32 default kernel with its loads issued at raised priority
   kVariantLongPrio = 92,          // fixed long keys: line-DMA kernel, DMA issued at raised priority
+  kVariantCsrLean2Scan1 = 93,     // csr lean2 (priority 1) with the class scan by wave 0 alone
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };

@@ -842,6 +842,7 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrLean2Prio ? 31
                          : variant == kVariantCsrLean2Prio3 ? 32
                          : variant == kVariantCsrLean2Prio1 ? 33
+                         : variant == kVariantCsrLean2Scan1 ? 34
                          : variant == kVariantCsrQueueProbeNoHash ? 28
                          : variant == kVariantCsrQueueProbeNoFeed ? 29
                          : variant == kVariantCsrDbufProbeNoHash ? 25
