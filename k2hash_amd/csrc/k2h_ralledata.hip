@@ -249,7 +249,9 @@ __device__ __forceinline__ void staged_key_hash(const uint8_t* end, uint32_t len
 // wrong offsets), 2: the same without the piece stores.  PU: pieces per loop trip;
 // SW0: the staged loads on all four waves (default: waves 1-3, so wave 0 only waits for its
 // records' offsets)
-template <bool FUSED, int PROBE = 0, int PU = 1, bool SW0 = false>
+// PRIO (lab): 1 = the loads (record offsets, span offsets, staged pieces) issued at raised
+// issue priority; 2 = all of phase 1 (loads and record work) at raised priority.
+template <bool FUSED, int PROBE = 0, int PU = 1, bool SW0 = false, int PRIO = 0>
 // 7 waves/SIMD (<= 72 VGPRs): the LDS image allows 7 blocks per CU
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void ralledata_gather_kernel(
     RalleInputs in, uint64_t n, const uint64_t* __restrict__ h, uint8_t* __restrict__ out,
@@ -264,6 +266,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
   const uint32_t tid = threadIdx.x;
   uint64_t t0 = 0, t1 = 0, t2 = 0, ta = 0, tb = 0;
   if constexpr (PROBE) t0 = __builtin_amdgcn_s_memtime();
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
   const uint64_t r0 = (uint64_t)blockIdx.x * R;
   const uint32_t nr = (uint32_t)(n - r0 < (uint64_t)R ? n - r0 : (uint64_t)R);
   const uint64_t* offs[4] = {in.koff, in.voff, in.soff, in.aoff};
@@ -332,6 +335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
       dst[u] = kGatherHdr + 80 * R + 16 * (uint32_t)q;
     }
   }
+  if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
   // 1b. one thread per record: header, segment table, piece table, blob offset.  All
   // block-relative quantities fit 32 bits once the spans fit the image.
   const uint64_t a_out = (uint64_t)(uintptr_t)(out + o_first);
@@ -386,6 +390,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
 #pragma unroll
   for (int u = 0; u < PPT; ++u)
     if (dst[u] != 0xffffffffu) *reinterpret_cast<u32x4_al*>(img + dst[u]) = v[u];
+  if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
   if constexpr (PROBE) t1 = __builtin_amdgcn_s_memtime();
   if constexpr (FUSED) {  // 1c. wave 0 hashes the block's keys from the image into the headers
@@ -699,6 +704,15 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
   if (variant == kVariantRalleStageAll) {
     ralledata_gather_kernel<true, 0, 1, true>
         <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+    return hipGetLastError();
+  }
+  if (variant == kVariantRallePrioLoads || variant == kVariantRallePrioPhase1) {
+    if (variant == kVariantRallePrioLoads)
+      ralledata_gather_kernel<true, 0, 1, false, 1>
+          <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+    else
+      ralledata_gather_kernel<true, 0, 1, false, 2>
+          <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
     return hipGetLastError();
   }
   if (variant == kVariantRallePieces2) {
