@@ -331,7 +331,7 @@ enum {
   kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
   kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
   kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30,
-  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34
+  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -863,12 +863,93 @@ __device__ __forceinline__ void pair_walk2(uint32_t k0, uint32_t p0, const uint8
   }
 }
 
+// Minimum over the wave (DPP: quad swaps, half-row and row mirrors, then the row
+// broadcasts; lanes whose source is masked keep their own value), read from lane 63.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ uint32_t dpp_min_step(uint32_t v) {
+  const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xf, false);
+  return o < v ? o : v;
+}
+__device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v) {
+  v = dpp_min_step<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
+  v = dpp_min_step<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
+  v = dpp_min_step<0x141, 0xf>(v);  // row_half_mirror
+  v = dpp_min_step<0x140, 0xf>(v);  // row_mirror
+  v = dpp_min_step<0x142, 0xa>(v);  // row_bcast:15
+  v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// Pair walk in unchecked runs (round 2, lab WALK 4): the same lane program as pair_walk
+// (key A's k0 chunks, then key B's k1), but instead of testing every step for the lane's
+// switch and end, the wave takes the minimum over its lanes of the next event (switch at
+// k0, end at k0 + k1), runs that many steps with a scalar counter only -- one address add
+// and one LDS read per step besides the hash -- and then handles the event for the lanes
+// that reached it.  With length-sorted pairs a wave sees only a handful of distinct event
+// steps.  Finished lanes keep hashing stage bytes (results dropped).
+__device__ __forceinline__ void pair_walk3(uint32_t k0, uint32_t p0, const uint8_t* cp0, uint32_t k1, uint32_t p1,
+                                           const uint8_t* cp1, const uint8_t* safe, const uint64_t* spad,
+                                           const uint4* masks, uint64_t& h0, uint64_t& h1v) {
+  constexpr uint32_t kNone = 0xFFFFFFFFu;
+  const uint32_t T = k0 + k1;
+  h0 = 0;
+  h1v = 0;
+  uint32_t ev = T == 0 ? kNone : (k1 ? k0 : T);
+  bool inB = false;
+  const uint8_t* base = T ? cp0 : safe;  // chunk t of the lane's program at base + 16 t
+  uint64_t st = spad[p0];
+  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32);
+  uint4 m = masks[p0];
+  uint4 c0 = ld16(base);
+  c0 = make_uint4(c0.x & m.x, c0.y & m.y, c0.z & m.z, c0.w & m.w);
+  uint32_t t = 0;  // wave-uniform step
+  for (;;) {
+    const uint32_t e = wave_min_dpp(ev);
+    if (e == kNone) break;
+    uint32_t run = e - t;
+    const uint8_t* q = base + 16u * t;  // chunk t
+    while (run >= 2) {
+      const uint4 c1 = ld16(q + 16);
+      fnv_chunk16<0>(lo, hi, c0);
+      c0 = ld16(q + 32);
+      fnv_chunk16<1>(lo, hi, c1);
+      q += 32;
+      run -= 2;
+    }
+    if (run) {
+      const uint4 c1 = ld16(q + 16);
+      fnv_chunk16<0>(lo, hi, c0);
+      c0 = c1;
+    }
+    t = e;
+    if (ev == t) {  // this lane's event
+      if (!inB && k1) {
+        h0 = pack2(lo, hi);
+        inB = true;
+        st = spad[p1];
+        lo = (uint32_t)st;
+        hi = (uint32_t)(st >> 32);
+        base = cp1 - 16 * (int32_t)t;
+        m = masks[p1];
+        c0 = ld16(cp1);
+        c0 = make_uint4(c0.x & m.x, c0.y & m.y, c0.z & m.z, c0.w & m.w);
+        ev = T;
+      } else {
+        if (inB) h1v = pack2(lo, hi);
+        else h0 = pack2(lo, hi);
+        ev = kNone;
+        base = safe - 16 * (int32_t)t;
+      }
+    }
+  }
+}
+
 // CLK (lab clock probe, H2 false): h2 receives per wave the shader-clock / 100 MHz stamps
 // at entry and after the hash (tools/clock_probe.py).  PRIO (lab): the load / sort phase at
 // raised issue priority, back to normal for the hash walk, so a tile's setup is not queued
 // behind the other block's hash instructions on the same SIMD.
 // SCAN1 (lab): the 128-class scan by wave 0 alone, two classes per lane (one barrier fewer).
-template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0, bool SCAN1 = false>
+template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0, bool SCAN1 = false, bool WALK4 = false>
 __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
                                                             SpadTable spad_tab, uint64_t* __restrict__ h1,
@@ -994,8 +1075,12 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
     const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
     const bool only_b = kA == 0;  // key A empty (or absent): walk B alone
     uint64_t hw0, hw1;
-    pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
-              hw0, hw1);
+    if constexpr (WALK4)
+      pair_walk3(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
+                 s_spad, s_mask, hw0, hw1);
+    else
+      pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
+                hw0, hw1);
     const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
     if (has_a) {
       h1[t0 + ka] = hA;
@@ -1991,7 +2076,7 @@ template <int PROBE = 0, bool QUEUE = false>
 }
 
 // lean2 with its load / sort phase at issue priority PRIO (lab A/B)
-template <int PRIO, bool SCAN1 = false>
+template <int PRIO, bool SCAN1 = false, bool WALK4 = false>
 [[maybe_unused]] static hipError_t launch_lean2_prio(const uint8_t* bb, const uint64_t* offsets, uint64_t n,
                                                      const SpadTable& t, uint64_t* h1, uint64_t* h2, hipStream_t stream) {
   const unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
@@ -2002,10 +2087,10 @@ template <int PRIO, bool SCAN1 = false>
   e = hipMemsetAsync(scratch, 0, 4, stream);
   if (e == hipSuccess) {
     if (h2) {
-      fnv_csr_lean2_kernel<true, false, 3, false, PRIO, SCAN1><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<true, false, 3, false, PRIO, SCAN1, WALK4><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
       fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
     } else {
-      fnv_csr_lean2_kernel<false, false, 3, false, PRIO, SCAN1><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<false, false, 3, false, PRIO, SCAN1, WALK4><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
       fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
     }
     e = hipGetLastError();
@@ -2024,6 +2109,7 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeLean2Prio) return launch_lean2_prio<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio3) return launch_lean2_prio<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2Runs) return launch_lean2_prio<1, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Scan1) return launch_lean2_prio<1, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio1) return launch_lean2_prio<1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeQueuePrio) return launch_dbuf<3, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
