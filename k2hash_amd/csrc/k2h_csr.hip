@@ -331,7 +331,7 @@ enum {
   kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
   kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
   kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30,
-  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35
+  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -1122,6 +1122,195 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
       if constexpr (H2) h2[t0 + k] = r2;
       if constexpr (EPI) bucket_emit<false>(bp, t0 + k, r1);
     }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// CSR lean3 (round 2, lab): lean2 made persistent, with the NEXT tile's offsets fetched by
+// LDS-DMA into 2.5 KiB of spare LDS while the current tile is sorted and hashed (two lean2
+// blocks leave ~8 KiB of a CU's 160 KiB free).  A tile then starts from offsets already in
+// LDS -- no HBM round trip before its span DMA -- and no registers hold the prefetch (the
+// register-prefetch persistent form, pair variant 63, lost to its VGPR and wait cost).
+// Only the low words of the 513 offsets are fetched (tile-relative offsets are 32-bit),
+// plus the high words of the first and end offsets.  The span DMA is waited for with a
+// counted vmcnt that leaves the prefetch in flight (every wave issues exactly 3 prefetch
+// loads after its span pieces).
+// ---------------------------------------------------------------------------
+template <bool H2, bool EPI = false>
+__global__ __launch_bounds__(256) void fnv_csr_lean3_kernel(const uint8_t* __restrict__ bytes,
+                                                            const uint64_t* __restrict__ offsets, uint64_t n,
+                                                            SpadTable spad_tab, uint64_t* __restrict__ h1,
+                                                            uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
+                                                            uint32_t* __restrict__ over_count, BucketParams bp = {}) {
+  constexpr uint32_t TK = 512, NW = 4, NT = 256, NB = 128;
+  constexpr uint32_t kStage = 72 * 1024u;
+  __shared__ uint32_t s_rel[TK + 1];
+  __shared__ uint16_t s_order[TK];
+  __shared__ uint32_t s_hist[NB];
+  __shared__ uint64_t s_spad[16];
+  __shared__ uint4 s_mask[16];
+  __shared__ __attribute__((aligned(16))) uint32_t s_nlo[9 * 64];  // next tile: low words of offsets t0 .. t0+512
+  __shared__ __attribute__((aligned(16))) uint32_t s_nhi[3 * 64];  // [0] / [1]: high words of its first / end offset
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[16 + kStage];
+
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint64_t ntiles = (n + TK - 1) / TK;
+  const uint64_t stride = gridDim.x;
+  uint64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  if (tid < 16) {
+    s_spad[tid] = spad_tab.v[tid];
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
+      int32_t sh = 8 * ((int32_t)tid - 4 * i);
+      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
+    }
+    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
+  // the offsets of tile tl into s_nlo / s_nhi: 12 dword rows of 64 lanes, 3 per wave (rows
+  // 9-11: the two high words, then re-reads); lanes past the tile's end offset re-read it
+  auto prefetch = [&](uint64_t tl) {
+    const uint64_t u0 = tl * TK;
+    const uint32_t c = (uint32_t)(n - u0 < (uint64_t)TK ? n - u0 : (uint64_t)TK);
+#pragma unroll
+    for (uint32_t r = 0; r < 3; ++r) {
+      const uint32_t row = wave + NW * r;  // 0..11
+      const uint32_t k = 64u * row + lane;
+      const uint32_t* src;
+      uint32_t* dst;
+      if (row < 9) {
+        src = off32 + 2 * (u0 + (k < c ? k : c));
+        dst = s_nlo + 64u * row;
+      } else {
+        src = off32 + 2 * (u0 + (lane == 0 ? 0u : c)) + 1;  // high words
+        dst = s_nhi + 64u * (row - 9);
+      }
+      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
+    }
+  };
+  // The hashes of a tile are stored after the NEXT tile's setup (deferred): at the top of
+  // the loop only the prefetched offsets are outstanding, so a full vmcnt(0) there costs no
+  // wait for the previous tile's stores.
+  static_assert(!EPI, "lab kernel");
+  bool pend_a = false, pend_b = false;
+  uint64_t pt0 = 0, pha = 0, phb = 0, pha2 = 0, phb2 = 0;
+  uint32_t pka = 0, pkb = 0;
+  auto flush = [&]() {
+    if (pend_a) {
+      h1[pt0 + pka] = pha;
+      if constexpr (H2) h2[pt0 + pka] = pha2;
+    }
+    if (pend_b) {
+      h1[pt0 + pkb] = phb;
+      if constexpr (H2) h2[pt0 + pkb] = phb2;
+    }
+    pend_a = pend_b = false;
+  };
+  prefetch(tile);
+  for (;;) {
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this tile's offsets have landed
+    lds_barrier();
+    __builtin_amdgcn_s_setprio(1);
+    const uint64_t t0 = tile * TK;
+    const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
+    const uint32_t lo0 = s_nlo[0], loN = s_nlo[cnt];
+    const uint64_t o0 = ((uint64_t)s_nhi[0] << 32) | lo0, oN = ((uint64_t)s_nhi[1] << 32) | loN;
+    const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
+    const uint64_t span_lo = kb & ~15ull;
+    const uint32_t delta = (uint32_t)(kb & 15u);
+    const uint64_t span = oN - o0 + delta;
+    const uint64_t next = tile + stride;
+    const bool more = next < ntiles;
+    for (uint32_t k = tid; k <= cnt; k += NT) s_rel[k] = s_nlo[k] - lo0;
+    if (tid < NB) s_hist[tid] = 0;
+    lds_barrier();  // s_rel in; s_nlo / s_nhi consumed
+    flush();        // the previous tile's hashes
+    if (span > kStage) {  // block-uniform: the ring kernel hashes this tile
+      if (tid == 0) over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
+      if (!more) return;
+      prefetch(next);
+      tile = next;
+      continue;
+    }
+    if (oN > o0) {
+      const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
+      const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
+      const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
+      uint32_t off = 1024u * wave + 16u * lane;
+      for (uint32_t c = wave; c < npieces; c += NW, off += 1024u * NW) {
+        const uint32_t o = off < lastp ? off : lastp;
+        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
+                                         (__attribute__((address_space(3))) void*)(s_stage + 16 + 1024u * c), 16, 0, 0);
+      }
+    }
+    if (more) prefetch(next);
+    constexpr uint32_t KPT = (TK + NT - 1) / NT;
+    uint32_t bins[KPT];
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; ++j) {
+      uint32_t k = tid + NT * j;
+      if (k < cnt) {
+        bins[j] = len_bin128_32(s_rel[k + 1] - s_rel[k]);
+        lds_add(&s_hist[bins[j]], 1u);
+      }
+    }
+    lds_barrier();
+    if (wave == 0) {
+      const uint32_t v0 = s_hist[2 * lane], v1 = s_hist[2 * lane + 1], sum = v0 + v1;
+      uint32_t incl = sum;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= (uint32_t)d) incl += y;
+      }
+      s_hist[2 * lane] = incl - sum;
+      s_hist[2 * lane + 1] = incl - sum + v0;
+    }
+    lds_barrier();
+#pragma unroll
+    for (uint32_t j = 0; j < KPT; ++j) {
+      uint32_t k = tid + NT * j;
+      if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
+    }
+    // this wave's span pieces have landed (its 3 prefetch loads, issued after them, may not)
+    if (more) __builtin_amdgcn_s_waitcnt(0x0F73);  // vmcnt(3)
+    else __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0)
+    lds_barrier();  // ... and every other wave's
+    __builtin_amdgcn_s_setprio(0);
+    const uint8_t* key0 = s_stage + 16 + delta;
+    const uint32_t i = wave * 64u + lane;
+    const bool has_a = i < (cnt + 1u) / 2u, has_b = i < cnt / 2u;
+    const uint32_t ka = s_order[has_a ? i : 0u], kbi = s_order[has_b ? cnt - 1u - i : 0u];
+    const uint32_t ra = s_rel[ka], rae = s_rel[ka + 1], rb = s_rel[kbi], rbe = s_rel[kbi + 1];
+    const uint32_t la = has_a ? rae - ra : 0u, lb = has_b ? rbe - rb : 0u;
+    const uint32_t kA = (la + 15u) >> 4, kB = (lb + 15u) >> 4;
+    const uint32_t pA = (0u - la) & 15u, pB = (0u - lb) & 15u;
+    const uint8_t* cpA = key0 + (int32_t)(rae - 16u * kA);
+    const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
+    const bool only_b = kA == 0;
+    uint64_t hw0, hw1;
+    pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
+              hw0, hw1);
+    pha = kA ? hw0 : 0;
+    phb = kB ? (only_b ? hw0 : hw1) : 0;
+    if constexpr (H2) {
+      pha2 = second_from_first(pha, la, key0 + rae);
+      phb2 = second_from_first(phb, lb, key0 + rbe);
+    }
+    pt0 = t0;
+    pka = ka;
+    pkb = kbi;
+    pend_a = has_a;
+    pend_b = has_b;
+    if (!more) {
+      flush();
+      return;
+    }
+    tile = next;
   }
 }
 
@@ -2099,6 +2288,32 @@ template <int PRIO, bool SCAN1 = false, bool WALK4 = false>
   return e != hipSuccess ? e : f;
 }
 
+// persistent lean3 (lab A/B)
+[[maybe_unused]] static hipError_t launch_lean3(const uint8_t* bb, const uint64_t* offsets, uint64_t n, const SpadTable& t,
+                                                uint64_t* h1, uint64_t* h2, hipStream_t stream) {
+  const uint64_t ntiles = (n + kTileKeys - 1) / kTileKeys;
+  if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
+  uint32_t* scratch = nullptr;
+  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (ntiles + 1), stream);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(scratch, 0, 4, stream);
+  if (e == hipSuccess) {
+    if (h2) {
+      constexpr auto k = fnv_csr_lean3_kernel<true>;
+      k<<<resident_grid<k>(256, (unsigned)ntiles), 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch, BucketParams{});
+      fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
+    } else {
+      constexpr auto k = fnv_csr_lean3_kernel<false>;
+      k<<<resident_grid<k>(256, (unsigned)ntiles), 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch, BucketParams{});
+      fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+    }
+    e = hipGetLastError();
+  }
+  hipError_t f = hipFreeAsync(scratch, stream);
+  return e != hipSuccess ? e : f;
+}
+
 #if K2H_AMD_LAB
 static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
@@ -2109,6 +2324,7 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeLean2Prio) return launch_lean2_prio<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio3) return launch_lean2_prio<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean3) return launch_lean3((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Runs) return launch_lean2_prio<1, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Scan1) return launch_lean2_prio<1, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio1) return launch_lean2_prio<1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);

@@ -117,6 +117,7 @@ enum {
   kVariantRallePrioLoads = 94,    // ralledata gather: loads at raised issue priority / all of phase 1 at raised priority
   kVariantRallePrioPhase1 = 95,
   kVariantCsrLean2Runs = 96,      // csr lean2 (priority 1, one-wave scan) with the pair walk in unchecked runs
+  kVariantCsrLean3 = 97,          // csr lean3: persistent lean2, next tile's offsets LDS-DMA'd during the hash
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };

@@ -844,6 +844,7 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrLean2Prio1 ? 33
                          : variant == kVariantCsrLean2Scan1 ? 34
                          : variant == kVariantCsrLean2Runs ? 35
+                         : variant == kVariantCsrLean3 ? 36
                          : variant == kVariantCsrQueueProbeNoHash ? 28
                          : variant == kVariantCsrQueueProbeNoFeed ? 29
                          : variant == kVariantCsrDbufProbeNoHash ? 25
