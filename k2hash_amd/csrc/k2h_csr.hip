@@ -331,7 +331,7 @@ enum {
   kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
   kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
   kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30,
-  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36
+  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36, kModeLean2Desync1 = 37, kModeLean2Desync2 = 38
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -949,12 +949,14 @@ __device__ __forceinline__ void pair_walk3(uint32_t k0, uint32_t p0, const uint8
 // raised issue priority, back to normal for the hash walk, so a tile's setup is not queued
 // behind the other block's hash instructions on the same SIMD.
 // SCAN1 (lab): the 128-class scan by wave 0 alone, two classes per lane (one barrier fewer).
-template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0, bool SCAN1 = false, bool WALK4 = false>
+template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0, bool SCAN1 = false, bool WALK4 = false,
+          int DESYNC = 0>
 __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
                                                             SpadTable spad_tab, uint64_t* __restrict__ h1,
                                                             uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
-                                                            uint32_t* __restrict__ over_count, BucketParams bp = {}) {
+                                                            uint32_t* __restrict__ over_count, BucketParams bp = {},
+                                                            uint32_t ncu = 0) {
   constexpr uint32_t TK = 512, NW = 4, NT = 256, NB = 128;
   constexpr uint32_t kStage = 72 * 1024u;
   __shared__ uint32_t s_rel[TK + 1];
@@ -973,8 +975,20 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
   if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t t0 = (uint64_t)blockIdx.x * TK;
-  const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
+  // DESYNC (lab; ncu = CU count): some blocks of the first wave take half tiles, so the two
+  // tiles resident on a CU start half a tile apart (1: blocks [0, ncu); 2: even blocks of
+  // [0, 2 ncu)).  Measured: no change (the one-shot grid's turnover already desyncs them).
+  const uint64_t bx = blockIdx.x, C = ncu;
+  uint64_t t0 = bx * TK;
+  uint32_t tk = TK;
+  if constexpr (DESYNC == 1) {
+    t0 = bx < C ? bx * (TK / 2) : C * (TK / 2) + (bx - C) * TK;
+    tk = bx < C ? TK / 2 : TK;
+  } else if constexpr (DESYNC == 2) {
+    t0 = bx < 2 * C ? (bx / 2) * (TK + TK / 2) + ((bx & 1) ? TK / 2 : 0) : C * (TK + TK / 2) + (bx - 2 * C) * TK;
+    tk = (bx < 2 * C && !(bx & 1)) ? TK / 2 : TK;
+  }
+  const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)tk ? n - t0 : (uint64_t)tk);
   const uint64_t o0 = offsets[t0], oN = offsets[t0 + cnt];  // block-uniform
   const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
   const uint64_t span_lo = kb & ~15ull;
@@ -2265,10 +2279,17 @@ template <int PROBE = 0, bool QUEUE = false>
 }
 
 // lean2 with its load / sort phase at issue priority PRIO (lab A/B)
-template <int PRIO, bool SCAN1 = false, bool WALK4 = false>
+template <int PRIO, bool SCAN1 = false, bool WALK4 = false, int DESYNC = 0>
 [[maybe_unused]] static hipError_t launch_lean2_prio(const uint8_t* bb, const uint64_t* offsets, uint64_t n,
                                                      const SpadTable& t, uint64_t* h1, uint64_t* h2, hipStream_t stream) {
-  const unsigned g = (unsigned)((n + kTileKeys - 1) / kTileKeys);
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+  const uint64_t C = (uint64_t)cus;
+  // halves: C half tiles (desync 1) or C half + C full in the first 2C blocks (desync 2)
+  const uint64_t lead = DESYNC == 1 ? C * (kTileKeys / 2) : DESYNC == 2 ? C * (kTileKeys + kTileKeys / 2) : 0;
+  const uint64_t nlead = DESYNC == 1 ? C : DESYNC == 2 ? 2 * C : 0;
+  if (DESYNC && n <= lead) return hipErrorInvalidValue;  // lab: large inputs only
+  const unsigned g = DESYNC ? (unsigned)(nlead + (n - lead + kTileKeys - 1) / kTileKeys) : (unsigned)((n + kTileKeys - 1) / kTileKeys);
   const unsigned gl = g < 512u ? g : 512u;
   uint32_t* scratch = nullptr;
   hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (g + 1), stream);
@@ -2276,10 +2297,10 @@ template <int PRIO, bool SCAN1 = false, bool WALK4 = false>
   e = hipMemsetAsync(scratch, 0, 4, stream);
   if (e == hipSuccess) {
     if (h2) {
-      fnv_csr_lean2_kernel<true, false, 3, false, PRIO, SCAN1, WALK4><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<true, false, 3, false, PRIO, SCAN1, WALK4, DESYNC><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch, BucketParams{}, (uint32_t)cus);
       fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
     } else {
-      fnv_csr_lean2_kernel<false, false, 3, false, PRIO, SCAN1, WALK4><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+      fnv_csr_lean2_kernel<false, false, 3, false, PRIO, SCAN1, WALK4, DESYNC><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch, BucketParams{}, (uint32_t)cus);
       fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
     }
     e = hipGetLastError();
@@ -2324,6 +2345,8 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeLean2Prio) return launch_lean2_prio<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio3) return launch_lean2_prio<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2Desync1) return launch_lean2_prio<1, true, false, 1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2Desync2) return launch_lean2_prio<1, true, false, 2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean3) return launch_lean3((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Runs) return launch_lean2_prio<1, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Scan1) return launch_lean2_prio<1, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);

@@ -845,6 +845,8 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrLean2Scan1 ? 34
                          : variant == kVariantCsrLean2Runs ? 35
                          : variant == kVariantCsrLean3 ? 36
+                         : variant == kVariantCsrLean2Desync1 ? 37
+                         : variant == kVariantCsrLean2Desync2 ? 38
                          : variant == kVariantCsrQueueProbeNoHash ? 28
                          : variant == kVariantCsrQueueProbeNoFeed ? 29
                          : variant == kVariantCsrDbufProbeNoHash ? 25
