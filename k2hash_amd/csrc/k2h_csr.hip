@@ -331,7 +331,7 @@ enum {
   kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
   kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
   kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30,
-  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36, kModeLean2Desync1 = 37, kModeLean2Desync2 = 38
+  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36, kModeLean2Desync1 = 37, kModeLean2Desync2 = 38, kModeQueue320 = 39
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -388,9 +388,10 @@ __device__ __forceinline__ void csr_tile(uint64_t tile, const uint8_t* __restric
 
   K2H_PROF_STAMP(10)
   // 1. histogram of length classes
-  uint32_t bins[TK / 256];
+  constexpr int KPT = (TK + 255) / 256;  // keys per thread (TK need not be a multiple of 256)
+  uint32_t bins[KPT];
 #pragma unroll
-  for (int j = 0; j < TK / 256; ++j) {
+  for (int j = 0; j < KPT; ++j) {
     uint32_t k = tid + 256u * j;
     if (k < cnt) {
       bins[j] = len_bin(s_off[k + 1] - s_off[k]);
@@ -415,7 +416,7 @@ __device__ __forceinline__ void csr_tile(uint64_t tile, const uint8_t* __restric
   K2H_PROF_STAMP(12)
   // 3. scatter key indices in class order
 #pragma unroll
-  for (int j = 0; j < TK / 256; ++j) {
+  for (int j = 0; j < KPT; ++j) {
     uint32_t k = tid + 256u * j;
     if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
   }
@@ -1777,19 +1778,21 @@ __device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t target) 
 // PROBE (lab timing probes, wrong hashes): 1 = hash waves claim groups without hashing,
 // 2 = feeders stage the first two tiles only (later tiles re-hash stale slots);
 // 3 (correct hashes) = feeder waves at raised issue priority.
-template <bool H2, bool EPI = false, int PROBE = 0>
+// TK_ keys per tile (a multiple of 64, <= 512), NSLOT tile slots of STAGE_KIB KiB.
+template <bool H2, bool EPI = false, int PROBE = 0, int TK_ = 512, int NSLOT = 2, int STAGE_KIB = 72>
 __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
                                                             SpadTable spad_tab, uint64_t* __restrict__ h1,
                                                             uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
                                                             uint32_t* __restrict__ over_count, BucketParams bp = {}) {
-  constexpr uint32_t TK = 512, NB = 128, NH = 8, NDMA = 3, NF = 1 + NDMA;
-  constexpr uint32_t kStage = 72 * 1024u;
+  constexpr uint32_t TK = TK_, NB = 128, NH = 8, NDMA = 3, NF = 1 + NDMA, NQ = TK / 64;
+  static_assert(TK % 64 == 0 && TK <= 512, "whole rows of 64 keys");
+  constexpr uint32_t kStage = STAGE_KIB * 1024u;
   constexpr uint32_t kSlot = 16 + kStage + 1024u;  // + the overhang of the span's last 1 KiB DMA piece
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[2 * kSlot];
-  __shared__ uint32_t s_rel[2 * (TK + 1)];
-  __shared__ uint16_t s_order[2 * TK];
-  __shared__ uint32_t s_ctl[16];
+  __shared__ __attribute__((aligned(16))) uint8_t s_stage[NSLOT * kSlot];
+  __shared__ uint32_t s_rel[NSLOT * (TK + 1)];
+  __shared__ uint16_t s_order[NSLOT * TK];
+  __shared__ uint32_t s_ctl[8 * NSLOT];
   __shared__ uint32_t s_hist[NB];
   __shared__ uint64_t s_spad[16];
   __shared__ uint4 s_mask[16];
@@ -1808,8 +1811,9 @@ __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __res
       w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
     }
     s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
-    s_ctl[tid] = 0;
+    if (tid < 8 * NSLOT) s_ctl[tid] = 0;
   }
+  if (tid >= 16 && tid < 8 * NSLOT) s_ctl[tid] = 0;
   __syncthreads();
   auto tile_cnt = [n](uint64_t t0) -> uint32_t { return (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK); };
   auto rfl64 = [](uint64_t v) -> uint64_t {
@@ -1819,18 +1823,18 @@ __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __res
   };
   // a feeder wave's part of tile j is in LDS: count it; the last of the NF publishes the slot
   auto feeder_done = [&](uint32_t j) {
-    uint32_t* ctl = s_ctl + 8u * (j & 1u);
+    uint32_t* ctl = s_ctl + 8u * (j % NSLOT);
     uint32_t old = 0;
     if (lane == 0) old = lds_add_rtn(&ctl[3], 1u);
     old = __builtin_amdgcn_readfirstlane(old);
-    if (old == NF * ((j >> 1) + 1u) - 1u && lane == 0)
+    if (old == NF * (j / NSLOT + 1u) - 1u && lane == 0)
       asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_u32addr(&ctl[0])), "v"(j + 1u) : "memory");
   };
   const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
 
   if (wave < NH) {  // ---- hash waves ----
     for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t b = j & 1u;
+      const uint32_t b = j % NSLOT;
       uint32_t* ctl = s_ctl + 8u * b;
       lds_wait_ge(&ctl[0], j + 1u);
       const uint32_t cnt = lds_poll(&ctl[4]);
@@ -1866,7 +1870,7 @@ __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __res
   // the feeders issue ahead of the hash waves sharing their SIMD (PROBE 3)
   if constexpr (PROBE == 3) __builtin_amdgcn_s_setprio(3);
   if (wave == NH) {  // ---- sort wave: offsets, length classes, order, tile info ----
-    uint32_t pa[9];
+    uint32_t pa[NQ + 1];
     uint64_t pz = 0, pe = 0;
     // (per-lane vector loads through an index the compiler cannot see is zero: no scalar
     // loads, whose out-of-order return would turn every LDS wait into lgkmcnt(0))
@@ -1876,7 +1880,7 @@ __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __res
       uint32_t zero = 0;
       asm volatile("" : "+v"(zero));
 #pragma unroll
-      for (uint32_t q = 0; q < 9; ++q) {
+      for (uint32_t q = 0; q < NQ + 1; ++q) {
         const uint32_t k = lane + 64u * q;
         pa[q] = off32[2 * (t0 + (k < cnt ? k : cnt) + zero)];
       }
@@ -1885,20 +1889,20 @@ __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __res
     };
     if (J) fetch(first);
     for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t b = j & 1u;
+      const uint32_t b = j % NSLOT;
       uint32_t* ctl = s_ctl + 8u * b;
       const uint64_t tile = first + (uint64_t)j * stride, t0 = tile * TK;
       const uint32_t cnt = tile_cnt(t0);
       const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
-      uint32_t cur[9];
+      uint32_t cur[NQ + 1];
 #pragma unroll
-      for (uint32_t q = 0; q < 9; ++q) cur[q] = pa[q] - (uint32_t)o0;
+      for (uint32_t q = 0; q < NQ + 1; ++q) cur[q] = pa[q] - (uint32_t)o0;
       if (j + 1 < J) fetch(tile + stride);
       const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
       const uint32_t delta = (uint32_t)(kb & 15u);
       const uint64_t span = oN - o0 + delta;
-      lds_wait_ge(&ctl[2], NH * (j >> 1));  // every hash wave has left the slot's previous tile
-      if (PROBE == 2 && j >= 2) {
+      lds_wait_ge(&ctl[2], NH * (j / NSLOT));  // every hash wave has left the slot's previous tile
+      if (PROBE == 2 && j >= NSLOT) {
         if (lane == 0) ctl[1] = 0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         feeder_done(j);
@@ -1911,15 +1915,15 @@ __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __res
         if (lane == 0) over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
       } else {
 #pragma unroll
-        for (uint32_t q = 0; q < 9; ++q) {
+        for (uint32_t q = 0; q < NQ + 1; ++q) {
           const uint32_t k = lane + 64u * q;
           if (k <= cnt) rel[k] = cur[q];
         }
         s_hist[lane] = 0;
         s_hist[lane + 64] = 0;
-        uint32_t bins[8];
+        uint32_t bins[NQ];
 #pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
+        for (uint32_t q = 0; q < NQ; ++q) {
           const uint32_t k = lane + 64u * q;
           // key k's end offset: the next lane's value (lane 63: lane 0 of the next row);
           // taken with every lane active
@@ -1940,7 +1944,7 @@ __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __res
         s_hist[2 * lane + 1] = incl - sum + v0;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
+        for (uint32_t q = 0; q < NQ; ++q) {
           const uint32_t k = lane + 64u * q;
           if (k < cnt) ord[lds_add_rtn(&s_hist[bins[q]], 1u)] = (uint16_t)k;
         }
@@ -1970,15 +1974,15 @@ __global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __res
     };
     if (J) fetch(first);
     for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t b = j & 1u;
+      const uint32_t b = j % NSLOT;
       const uint64_t tile = first + (uint64_t)j * stride;
       const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
       if (j + 1 < J) fetch(tile + stride);
       const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
       const uint64_t span_lo = kb & ~15ull;
       const uint64_t span = oN - o0 + (kb & 15u);
-      lds_wait_ge(&s_ctl[8u * b + 2u], NH * (j >> 1));  // the slot's previous tile is consumed
-      if (span <= kStage && oN > o0 && !(PROBE == 2 && j >= 2)) {
+      lds_wait_ge(&s_ctl[8u * b + 2u], NH * (j / NSLOT));  // the slot's previous tile is consumed
+      if (span <= kStage && oN > o0 && !(PROBE == 2 && j >= NSLOT)) {
         // 1 KiB pieces, 16 B per lane; lanes past the span re-read its last 16 B into
         // stage bytes nobody reads
         const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
@@ -2335,6 +2339,33 @@ template <int PRIO, bool SCAN1 = false, bool WALK4 = false, int DESYNC = 0>
   return e != hipSuccess ? e : f;
 }
 
+// queue tiles of 320 keys in three 46 KiB slots, feeders at raised priority (lab A/B)
+[[maybe_unused]] static hipError_t launch_queue320(const uint8_t* bb, const uint64_t* offsets, uint64_t n, const SpadTable& t,
+                                                   uint64_t* h1, uint64_t* h2, hipStream_t stream) {
+  constexpr uint64_t TK = 320;
+  const uint64_t ntiles = (n + TK - 1) / TK;
+  if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
+  uint32_t* scratch = nullptr;
+  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (ntiles + 1), stream);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(scratch, 0, 4, stream);
+  if (e == hipSuccess) {
+    if (h2) {
+      constexpr auto k = fnv_csr_queue_kernel<true, false, 3, 320, 3, 46>;
+      k<<<resident_grid<k>(768, (unsigned)ntiles), 768, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch, BucketParams{});
+      fnv_csr_ring_list_kernel<true, false, 320><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
+    } else {
+      constexpr auto k = fnv_csr_queue_kernel<false, false, 3, 320, 3, 46>;
+      k<<<resident_grid<k>(768, (unsigned)ntiles), 768, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch, BucketParams{});
+      fnv_csr_ring_list_kernel<false, false, 320><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
+    }
+    e = hipGetLastError();
+  }
+  hipError_t f = hipFreeAsync(scratch, stream);
+  return e != hipSuccess ? e : f;
+}
+
 #if K2H_AMD_LAB
 static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
@@ -2345,6 +2376,7 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeLean2Prio) return launch_lean2_prio<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio3) return launch_lean2_prio<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeQueue320) return launch_queue320((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Desync1) return launch_lean2_prio<1, true, false, 1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Desync2) return launch_lean2_prio<1, true, false, 2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean3) return launch_lean3((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);

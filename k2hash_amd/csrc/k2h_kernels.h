@@ -120,6 +120,7 @@ enum {
   kVariantCsrLean3 = 97,          // csr lean3: persistent lean2, next tile's offsets LDS-DMA'd during the hash
   kVariantCsrLean2Desync1 = 98,   // csr lean2 (product settings), first-wave half tiles so co-resident tiles start out
   kVariantCsrLean2Desync2 = 99,   // of phase (98: blocks [0, #CU); 99: even blocks of [0, 2 #CU))
+  kVariantCsrQueue320 = 100,      // csr queue tiles of 320 keys in three 46 KiB slots, feeders at raised priority
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };
