@@ -864,86 +864,9 @@ __device__ __forceinline__ void pair_walk2(uint32_t k0, uint32_t p0, const uint8
   }
 }
 
-// Minimum over the wave (DPP: quad swaps, half-row and row mirrors, then the row
-// broadcasts; lanes whose source is masked keep their own value), read from lane 63.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ uint32_t dpp_min_step(uint32_t v) {
-  const uint32_t o = (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROW_MASK, 0xf, false);
-  return o < v ? o : v;
-}
-__device__ __forceinline__ uint32_t wave_min_dpp(uint32_t v) {
-  v = dpp_min_step<0xB1, 0xf>(v);   // quad_perm [1,0,3,2]
-  v = dpp_min_step<0x4E, 0xf>(v);   // quad_perm [2,3,0,1]
-  v = dpp_min_step<0x141, 0xf>(v);  // row_half_mirror
-  v = dpp_min_step<0x140, 0xf>(v);  // row_mirror
-  v = dpp_min_step<0x142, 0xa>(v);  // row_bcast:15
-  v = dpp_min_step<0x143, 0xc>(v);  // row_bcast:31
-  return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
-}
-
-// Pair walk in unchecked runs (round 2, lab WALK 4): the same lane program as pair_walk
-// (key A's k0 chunks, then key B's k1), but instead of testing every step for the lane's
-// switch and end, the wave takes the minimum over its lanes of the next event (switch at
-// k0, end at k0 + k1), runs that many steps with a scalar counter only -- one address add
-// and one LDS read per step besides the hash -- and then handles the event for the lanes
-// that reached it.  With length-sorted pairs a wave sees only a handful of distinct event
-// steps.  Finished lanes keep hashing stage bytes (results dropped).
-__device__ __forceinline__ void pair_walk3(uint32_t k0, uint32_t p0, const uint8_t* cp0, uint32_t k1, uint32_t p1,
-                                           const uint8_t* cp1, const uint8_t* safe, const uint64_t* spad,
-                                           const uint4* masks, uint64_t& h0, uint64_t& h1v) {
-  constexpr uint32_t kNone = 0xFFFFFFFFu;
-  const uint32_t T = k0 + k1;
-  h0 = 0;
-  h1v = 0;
-  uint32_t ev = T == 0 ? kNone : (k1 ? k0 : T);
-  bool inB = false;
-  const uint8_t* base = T ? cp0 : safe;  // chunk t of the lane's program at base + 16 t
-  uint64_t st = spad[p0];
-  uint32_t lo = (uint32_t)st, hi = (uint32_t)(st >> 32);
-  uint4 m = masks[p0];
-  uint4 c0 = ld16(base);
-  c0 = make_uint4(c0.x & m.x, c0.y & m.y, c0.z & m.z, c0.w & m.w);
-  uint32_t t = 0;  // wave-uniform step
-  for (;;) {
-    const uint32_t e = wave_min_dpp(ev);
-    if (e == kNone) break;
-    uint32_t run = e - t;
-    const uint8_t* q = base + 16u * t;  // chunk t
-    while (run >= 2) {
-      const uint4 c1 = ld16(q + 16);
-      fnv_chunk16<0>(lo, hi, c0);
-      c0 = ld16(q + 32);
-      fnv_chunk16<1>(lo, hi, c1);
-      q += 32;
-      run -= 2;
-    }
-    if (run) {
-      const uint4 c1 = ld16(q + 16);
-      fnv_chunk16<0>(lo, hi, c0);
-      c0 = c1;
-    }
-    t = e;
-    if (ev == t) {  // this lane's event
-      if (!inB && k1) {
-        h0 = pack2(lo, hi);
-        inB = true;
-        st = spad[p1];
-        lo = (uint32_t)st;
-        hi = (uint32_t)(st >> 32);
-        base = cp1 - 16 * (int32_t)t;
-        m = masks[p1];
-        c0 = ld16(cp1);
-        c0 = make_uint4(c0.x & m.x, c0.y & m.y, c0.z & m.z, c0.w & m.w);
-        ev = T;
-      } else {
-        if (inB) h1v = pack2(lo, hi);
-        else h0 = pack2(lo, hi);
-        ev = kNone;
-        base = safe - 16 * (int32_t)t;
-      }
-    }
-  }
-}
+#if K2H_AMD_LAB
+#include "k2h_csr_lab_walk.inc"
+#endif
 
 // CLK (lab clock probe, H2 false): h2 receives per wave the shader-clock / 100 MHz stamps
 // at entry and after the hash (tools/clock_probe.py).  PRIO (lab): the load / sort phase at
@@ -1090,10 +1013,12 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
     const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
     const bool only_b = kA == 0;  // key A empty (or absent): walk B alone
     uint64_t hw0, hw1;
+#if K2H_AMD_LAB
     if constexpr (WALK4)
       pair_walk3(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
                  s_spad, s_mask, hw0, hw1);
     else
+#endif
       pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
                 hw0, hw1);
     const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
@@ -1136,868 +1061,6 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
       h1[t0 + k] = r1;
       if constexpr (H2) h2[t0 + k] = r2;
       if constexpr (EPI) bucket_emit<false>(bp, t0 + k, r1);
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// CSR lean3 (round 2, lab): lean2 made persistent, with the NEXT tile's offsets fetched by
-// LDS-DMA into 2.5 KiB of spare LDS while the current tile is sorted and hashed (two lean2
-// blocks leave ~8 KiB of a CU's 160 KiB free).  A tile then starts from offsets already in
-// LDS -- no HBM round trip before its span DMA -- and no registers hold the prefetch (the
-// register-prefetch persistent form, pair variant 63, lost to its VGPR and wait cost).
-// Only the low words of the 513 offsets are fetched (tile-relative offsets are 32-bit),
-// plus the high words of the first and end offsets.  The span DMA is waited for with a
-// counted vmcnt that leaves the prefetch in flight (every wave issues exactly 3 prefetch
-// loads after its span pieces).
-// ---------------------------------------------------------------------------
-template <bool H2, bool EPI = false>
-__global__ __launch_bounds__(256) void fnv_csr_lean3_kernel(const uint8_t* __restrict__ bytes,
-                                                            const uint64_t* __restrict__ offsets, uint64_t n,
-                                                            SpadTable spad_tab, uint64_t* __restrict__ h1,
-                                                            uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
-                                                            uint32_t* __restrict__ over_count, BucketParams bp = {}) {
-  constexpr uint32_t TK = 512, NW = 4, NT = 256, NB = 128;
-  constexpr uint32_t kStage = 72 * 1024u;
-  __shared__ uint32_t s_rel[TK + 1];
-  __shared__ uint16_t s_order[TK];
-  __shared__ uint32_t s_hist[NB];
-  __shared__ uint64_t s_spad[16];
-  __shared__ uint4 s_mask[16];
-  __shared__ __attribute__((aligned(16))) uint32_t s_nlo[9 * 64];  // next tile: low words of offsets t0 .. t0+512
-  __shared__ __attribute__((aligned(16))) uint32_t s_nhi[3 * 64];  // [0] / [1]: high words of its first / end offset
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[16 + kStage];
-
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t ntiles = (n + TK - 1) / TK;
-  const uint64_t stride = gridDim.x;
-  uint64_t tile = blockIdx.x;
-  if (tile >= ntiles) return;
-  if (tid < 16) {
-    s_spad[tid] = spad_tab.v[tid];
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
-      int32_t sh = 8 * ((int32_t)tid - 4 * i);
-      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
-    }
-    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
-  // the offsets of tile tl into s_nlo / s_nhi: 12 dword rows of 64 lanes, 3 per wave (rows
-  // 9-11: the two high words, then re-reads); lanes past the tile's end offset re-read it
-  auto prefetch = [&](uint64_t tl) {
-    const uint64_t u0 = tl * TK;
-    const uint32_t c = (uint32_t)(n - u0 < (uint64_t)TK ? n - u0 : (uint64_t)TK);
-#pragma unroll
-    for (uint32_t r = 0; r < 3; ++r) {
-      const uint32_t row = wave + NW * r;  // 0..11
-      const uint32_t k = 64u * row + lane;
-      const uint32_t* src;
-      uint32_t* dst;
-      if (row < 9) {
-        src = off32 + 2 * (u0 + (k < c ? k : c));
-        dst = s_nlo + 64u * row;
-      } else {
-        src = off32 + 2 * (u0 + (lane == 0 ? 0u : c)) + 1;  // high words
-        dst = s_nhi + 64u * (row - 9);
-      }
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)dst, 4, 0, 0);
-    }
-  };
-  // The hashes of a tile are stored after the NEXT tile's setup (deferred): at the top of
-  // the loop only the prefetched offsets are outstanding, so a full vmcnt(0) there costs no
-  // wait for the previous tile's stores.
-  static_assert(!EPI, "lab kernel");
-  bool pend_a = false, pend_b = false;
-  uint64_t pt0 = 0, pha = 0, phb = 0, pha2 = 0, phb2 = 0;
-  uint32_t pka = 0, pkb = 0;
-  auto flush = [&]() {
-    if (pend_a) {
-      h1[pt0 + pka] = pha;
-      if constexpr (H2) h2[pt0 + pka] = pha2;
-    }
-    if (pend_b) {
-      h1[pt0 + pkb] = phb;
-      if constexpr (H2) h2[pt0 + pkb] = phb2;
-    }
-    pend_a = pend_b = false;
-  };
-  prefetch(tile);
-  for (;;) {
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0): this tile's offsets have landed
-    lds_barrier();
-    __builtin_amdgcn_s_setprio(1);
-    const uint64_t t0 = tile * TK;
-    const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
-    const uint32_t lo0 = s_nlo[0], loN = s_nlo[cnt];
-    const uint64_t o0 = ((uint64_t)s_nhi[0] << 32) | lo0, oN = ((uint64_t)s_nhi[1] << 32) | loN;
-    const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
-    const uint64_t span_lo = kb & ~15ull;
-    const uint32_t delta = (uint32_t)(kb & 15u);
-    const uint64_t span = oN - o0 + delta;
-    const uint64_t next = tile + stride;
-    const bool more = next < ntiles;
-    for (uint32_t k = tid; k <= cnt; k += NT) s_rel[k] = s_nlo[k] - lo0;
-    if (tid < NB) s_hist[tid] = 0;
-    lds_barrier();  // s_rel in; s_nlo / s_nhi consumed
-    flush();        // the previous tile's hashes
-    if (span > kStage) {  // block-uniform: the ring kernel hashes this tile
-      if (tid == 0) over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
-      if (!more) return;
-      prefetch(next);
-      tile = next;
-      continue;
-    }
-    if (oN > o0) {
-      const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
-      const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
-      const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
-      uint32_t off = 1024u * wave + 16u * lane;
-      for (uint32_t c = wave; c < npieces; c += NW, off += 1024u * NW) {
-        const uint32_t o = off < lastp ? off : lastp;
-        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
-                                         (__attribute__((address_space(3))) void*)(s_stage + 16 + 1024u * c), 16, 0, 0);
-      }
-    }
-    if (more) prefetch(next);
-    constexpr uint32_t KPT = (TK + NT - 1) / NT;
-    uint32_t bins[KPT];
-#pragma unroll
-    for (uint32_t j = 0; j < KPT; ++j) {
-      uint32_t k = tid + NT * j;
-      if (k < cnt) {
-        bins[j] = len_bin128_32(s_rel[k + 1] - s_rel[k]);
-        lds_add(&s_hist[bins[j]], 1u);
-      }
-    }
-    lds_barrier();
-    if (wave == 0) {
-      const uint32_t v0 = s_hist[2 * lane], v1 = s_hist[2 * lane + 1], sum = v0 + v1;
-      uint32_t incl = sum;
-#pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
-        uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= (uint32_t)d) incl += y;
-      }
-      s_hist[2 * lane] = incl - sum;
-      s_hist[2 * lane + 1] = incl - sum + v0;
-    }
-    lds_barrier();
-#pragma unroll
-    for (uint32_t j = 0; j < KPT; ++j) {
-      uint32_t k = tid + NT * j;
-      if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
-    }
-    // this wave's span pieces have landed (its 3 prefetch loads, issued after them, may not)
-    if (more) __builtin_amdgcn_s_waitcnt(0x0F73);  // vmcnt(3)
-    else __builtin_amdgcn_s_waitcnt(0x0F70);       // vmcnt(0)
-    lds_barrier();  // ... and every other wave's
-    __builtin_amdgcn_s_setprio(0);
-    const uint8_t* key0 = s_stage + 16 + delta;
-    const uint32_t i = wave * 64u + lane;
-    const bool has_a = i < (cnt + 1u) / 2u, has_b = i < cnt / 2u;
-    const uint32_t ka = s_order[has_a ? i : 0u], kbi = s_order[has_b ? cnt - 1u - i : 0u];
-    const uint32_t ra = s_rel[ka], rae = s_rel[ka + 1], rb = s_rel[kbi], rbe = s_rel[kbi + 1];
-    const uint32_t la = has_a ? rae - ra : 0u, lb = has_b ? rbe - rb : 0u;
-    const uint32_t kA = (la + 15u) >> 4, kB = (lb + 15u) >> 4;
-    const uint32_t pA = (0u - la) & 15u, pB = (0u - lb) & 15u;
-    const uint8_t* cpA = key0 + (int32_t)(rae - 16u * kA);
-    const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
-    const bool only_b = kA == 0;
-    uint64_t hw0, hw1;
-    pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
-              hw0, hw1);
-    pha = kA ? hw0 : 0;
-    phb = kB ? (only_b ? hw0 : hw1) : 0;
-    if constexpr (H2) {
-      pha2 = second_from_first(pha, la, key0 + rae);
-      phb2 = second_from_first(phb, lb, key0 + rbe);
-    }
-    pt0 = t0;
-    pka = ka;
-    pkb = kbi;
-    pend_a = has_a;
-    pend_b = has_b;
-    if (!more) {
-      flush();
-      return;
-    }
-    tile = next;
-  }
-}
-
-// ---------------------------------------------------------------------------
-// CSR pair tiles (round 2): TK = 128 NW keys per tile, NW waves, lane i of the block hashes
-// sorted keys i and TK-1-i back to back (pair_walk), the tile's bytes DMA'd into a
-// STAGE_KIB KiB LDS stage.  Compared with fnv_csr_lean2_kernel (512 keys, 4 waves, 72 KiB,
-// two blocks per CU):
-//  - smaller tiles fit more independent blocks per CU (NW = 2: 256 keys, 36 KiB, four
-//    blocks), so the blocks of a CU drift out of phase and one block's load / sort phase
-//    overlaps the others' hashing instead of all of them loading, then all hashing;
-//  - PERSIST: a grid of resident blocks walks the tiles with a stride, and each block
-//    loads the offsets of its next tile into registers before it starts hashing the
-//    current one, so the next tile starts without a round trip to HBM (1.6 us of a
-//    10.3 us tile life in round 1, profiles/r01f_csr_phases_sortfix.txt).
-// Tiles whose span exceeds the stage are listed for the ring kernel, as in lean2.
-// ---------------------------------------------------------------------------
-template <bool H2, bool EPI, int NW, int STAGE_KIB, bool PERSIST, bool STAGGER = false, bool W2 = false,
-          bool Z = false>
-__global__ __launch_bounds__(NW * 64) void fnv_csr_pair_kernel(const uint8_t* __restrict__ bytes,
-                                                               const uint64_t* __restrict__ offsets, uint64_t n,
-                                                               SpadTable spad_tab, uint64_t* __restrict__ h1,
-                                                               uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
-                                                               uint32_t* __restrict__ over_count, BucketParams bp = {}) {
-  constexpr uint32_t NT = NW * 64, TK = 2 * NT, NB = 128;
-  constexpr uint32_t kStage = STAGE_KIB * 1024u;
-  static_assert(NT >= NB || NB % NT == 0, "scan covers the length classes");
-  __shared__ uint32_t s_rel[TK + 1];
-  __shared__ uint16_t s_order[TK];
-  __shared__ uint32_t s_hist[NB];
-  __shared__ uint32_t s_wsum[NW];
-  __shared__ uint64_t s_spad[16];
-  __shared__ uint4 s_mask[16];
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[16 + kStage];
-
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t ntiles = (n + TK - 1) / TK;
-  uint64_t tile = blockIdx.x;
-  if (tid < 16) {
-    s_spad[tid] = spad_tab.v[tid];
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
-      int32_t sh = 8 * ((int32_t)tid - 4 * i);
-      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
-    }
-    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  // this thread's offsets of a tile: keys tid and tid + NT, and the tile's first / end offset
-  // (the same address in every lane: loaded per lane through an index the compiler cannot
-  // see is zero, so they are vector loads and not scalar loads, whose out-of-order return
-  // would make every LDS wait of the hash loop a full lgkmcnt(0) until they land)
-  // (a and b: only the low words -- the tile-relative offsets are 32-bit -- so no half of a
-  // pending load's destination is dead and reused, which would force a wait for it)
-  const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
-  auto fetch = [&](uint64_t t, uint32_t& a, uint32_t& b, uint64_t& z, uint64_t& e) {
-    const uint64_t t0 = t * TK;
-    const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
-    uint32_t zero = 0;
-    asm volatile("" : "+v"(zero));
-    a = off32[2 * (t0 + (tid < cnt ? tid : cnt))];
-    b = off32[2 * (t0 + (tid + NT < cnt ? tid + NT : cnt))];
-    z = offsets[t0 + zero];
-    e = offsets[t0 + cnt + zero];
-  };
-  uint32_t pa, pb;
-  uint64_t pz, pe;
-  fetch(tile, pa, pb, pz, pe);
-  if constexpr (PERSIST && STAGGER) {
-    // resident blocks start in lock step; the second half of the grid (the other blocks of
-    // each CU) starts about half a tile later, so one block's load / sort phase overlaps
-    // its neighbours' hashing instead of coinciding with it
-    if (blockIdx.x >= gridDim.x / 2)
-      for (int i = 0; i < 40; ++i) __builtin_amdgcn_s_sleep(127);
-  }
-  for (;;) {
-    const uint64_t t0 = tile * TK;
-    const uint32_t cnt = (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK);
-    const uint64_t o0 = pz, oN = pe;  // block-uniform
-    const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
-    const uint64_t span_lo = kb & ~15ull;
-    const uint32_t delta = (uint32_t)(kb & 15u);
-    const uint64_t span = oN - o0 + delta;  // stage bytes up to the tile's last key byte
-    const uint64_t next = tile + gridDim.x;
-    if (span > kStage) {  // block-uniform: the ring kernel hashes this tile
-      if (tid == 0) over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
-      if (!PERSIST || next >= ntiles) return;
-      tile = next;
-      fetch(tile, pa, pb, pz, pe);
-      continue;
-    }
-    if (tid < cnt) s_rel[tid] = pa - (uint32_t)o0;
-    if (tid + NT < cnt) s_rel[tid + NT] = pb - (uint32_t)o0;
-    if (tid == 0) s_rel[cnt] = (uint32_t)(oN - o0);
-    if (tid < NB) s_hist[tid] = 0;
-    // DMA of the tile span (16-byte pieces; pieces past the span re-read its last piece
-    // into stage bytes nobody reads), in flight during the sort
-    if (oN > o0) {
-      const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
-      const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
-      const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
-      uint32_t off = 1024u * wave + 16u * lane;
-      for (uint32_t c = wave; c < npieces; c += NW, off += 1024u * NW) {
-        const uint32_t o = off < lastp ? off : lastp;
-        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
-                                         (__attribute__((address_space(3))) void*)(s_stage + 16 + 1024u * c), 16, 0, 0);
-      }
-    }
-    lds_barrier();
-    uint32_t bins[2];
-#pragma unroll
-    for (uint32_t j = 0; j < 2; ++j) {
-      const uint32_t k = tid + NT * j;
-      if (k < cnt) {
-        bins[j] = len_bin128_32(s_rel[k + 1] - s_rel[k]);
-        lds_add(&s_hist[bins[j]], 1u);
-      }
-    }
-    lds_barrier();
-    // exclusive scan of the 128 class counts
-    uint32_t v = tid < NB ? s_hist[tid] : 0u, incl = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      uint32_t y = __shfl_up(incl, d, 64);
-      if (lane >= (uint32_t)d) incl += y;
-    }
-    if (lane == 63) s_wsum[wave] = incl;
-    lds_barrier();
-    uint32_t base = 0;
-    for (uint32_t w = 0; w < wave; ++w) base += s_wsum[w];
-    if (tid < NB) s_hist[tid] = base + incl - v;
-    lds_barrier();
-#pragma unroll
-    for (uint32_t j = 0; j < 2; ++j) {
-      const uint32_t k = tid + NT * j;
-      if (k < cnt) s_order[lds_add_rtn(&s_hist[bins[j]], 1u)] = (uint16_t)k;
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's DMA pieces have landed
-    lds_barrier();                                     // ... and every wave's
-    // The next tile's offsets, in flight while this one is hashed (PERSIST).  Issued after a
-    // first read of the stage: the compiler puts its own vmcnt(0) for the DMA'd object in
-    // front of that read, and must not put it after the prefetch (it would wait for it).
-    const bool more = PERSIST && next < ntiles;
-    if constexpr (PERSIST) {
-      const uint32_t touch = s_stage[16];
-      asm volatile("" ::"v"(touch) : "memory");
-      fetch(more ? next : tile, pa, pb, pz, pe);  // unconditional: no phi copies that would wait for it
-    }
-    const uint8_t* key0 = s_stage + 16 + delta;
-    {
-      const uint32_t i = tid;
-      const bool has_a = i < (cnt + 1u) / 2u, has_b = i < cnt / 2u;
-      const uint32_t ka = s_order[has_a ? i : 0u], kbi = s_order[has_b ? cnt - 1u - i : 0u];
-      const uint32_t ra = s_rel[ka], rae = s_rel[ka + 1], rb = s_rel[kbi], rbe = s_rel[kbi + 1];
-      const uint32_t la = has_a ? rae - ra : 0u, lb = has_b ? rbe - rb : 0u;
-      const uint32_t kA = (la + 15u) >> 4, kB = (lb + 15u) >> 4;
-      const uint32_t pA = (0u - la) & 15u, pB = (0u - lb) & 15u;
-      const uint8_t* cpA = key0 + (int32_t)(rae - 16u * kA);
-      const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
-      const bool only_b = kA == 0;  // key A empty (or absent): walk B alone
-      uint64_t hw0, hw1;
-      if constexpr (W2)
-        pair_walk2(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
-                   s_spad, s_mask, hw0, hw1);
-      else
-        pair_walk<Z>(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad,
-                     s_mask, hw0, hw1);
-      const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
-      if (has_a) {
-        h1[t0 + ka] = hA;
-        if constexpr (H2) h2[t0 + ka] = second_from_first(hA, la, key0 + rae);
-        if constexpr (EPI) bucket_emit<false>(bp, t0 + ka, hA);
-      }
-      if (has_b) {
-        h1[t0 + kbi] = hB;
-        if constexpr (H2) h2[t0 + kbi] = second_from_first(hB, lb, key0 + rbe);
-        if constexpr (EPI) bucket_emit<false>(bp, t0 + kbi, hB);
-      }
-    }
-    if (!more) return;
-    tile = next;
-    lds_barrier();  // every lane is done with the stage and the sort arrays
-  }
-}
-
-// ---------------------------------------------------------------------------
-// CSR double-buffered tiles (round 2).  One persistent 512-thread block per CU walks
-// the 512-key tiles blockIdx, blockIdx + grid, ...  with two LDS tile slots (stage,
-// tile-relative offsets, sorted order), and its waves split by role:
-//   waves 0-3  hash tile j from slot j&1 (pair walk, as fnv_csr_lean2_kernel WALK 3);
-//   wave 4     prepares tile j+1 in the other slot: offsets -> LDS, counting sort by
-//              chunk count (one wave, so no block barrier inside the sort), tile info;
-//   waves 5-7  DMA tile j+1's byte span into the other slot's stage.
-// One s_barrier per tile hands a prepared slot to the hash waves and the slot they
-// just finished to the feeders.  The feeders prefetch tile j+2's offsets into registers
-// during tile j+1's preparation, so the offset load, the sort and the span DMA -- 45 %
-// of a lean2 tile's life, during which its waves issued no hash work -- all run under
-// the hash of the previous tile.  Each role is its own loop: the hash waves' code never
-// follows a global_load_lds, so hipcc puts no vmcnt drain in front of their LDS reads.
-// Tiles whose span exceeds the stage go to the ring list, as in lean2.
-// PROBE (lab timing probes, wrong hashes): 1 = hash waves do not hash (feeder-bound
-// time), 2 = feeders prepare the first two tiles only (hash-bound time).
-// ---------------------------------------------------------------------------
-template <bool H2, bool EPI = false, int PROBE = 0>
-__global__ __launch_bounds__(512) void fnv_csr_dbuf_kernel(const uint8_t* __restrict__ bytes,
-                                                           const uint64_t* __restrict__ offsets, uint64_t n,
-                                                           SpadTable spad_tab, uint64_t* __restrict__ h1,
-                                                           uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
-                                                           uint32_t* __restrict__ over_count, BucketParams bp = {}) {
-  constexpr uint32_t TK = 512, NB = 128, NDMA = 3;
-  constexpr uint32_t kStage = 72 * 1024u;
-  constexpr uint32_t kSlot = 16 + kStage + 1024u;  // + the overhang of the span's last 1 KiB DMA piece
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[2 * kSlot];
-  __shared__ uint32_t s_rel[2 * (TK + 1)];
-  __shared__ uint16_t s_order[2 * TK];
-  __shared__ uint32_t s_info[4];  // per slot: key count (0 = not staged here), stage lead delta
-  __shared__ uint32_t s_hist[NB];
-  __shared__ uint64_t s_spad[16];
-  __shared__ uint4 s_mask[16];
-
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t ntiles = (n + TK - 1) / TK;
-  const uint64_t first = blockIdx.x, stride = gridDim.x;
-  const uint32_t J = first < ntiles ? (uint32_t)((ntiles - first + stride - 1) / stride) : 0u;
-  if (tid < 16) {
-    s_spad[tid] = spad_tab.v[tid];
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
-      int32_t sh = 8 * ((int32_t)tid - 4 * i);
-      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
-    }
-    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  __syncthreads();
-  auto tile_cnt = [n](uint64_t t0) -> uint32_t { return (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK); };
-  auto rfl64 = [](uint64_t v) -> uint64_t {
-    // (readfirstlane returns int: each half goes through uint32_t, or the low one sign-extends)
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-  };
-  const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
-
-  if (wave < 4) {  // ---- hash waves ----
-    for (uint32_t j = 0; j < J; ++j) {
-      lds_barrier();
-      const uint32_t b = j & 1u;
-      const uint32_t cnt = __builtin_amdgcn_readfirstlane(s_info[2 * b]);
-      if (cnt == 0) continue;
-      if constexpr (PROBE == 1) continue;
-      const uint32_t delta = __builtin_amdgcn_readfirstlane(s_info[2 * b + 1]);
-      const uint64_t t0 = (first + (uint64_t)j * stride) * TK;
-      const uint16_t* ord = s_order + b * TK;
-      const uint32_t* rel = s_rel + b * (TK + 1);
-      const uint8_t* key0 = s_stage + b * kSlot + 16 + delta;
-      const uint32_t i = tid;
-      const bool has_a = i < (cnt + 1u) / 2u, has_b = i < cnt / 2u;
-      const uint32_t ka = ord[has_a ? i : 0u], kbi = ord[has_b ? cnt - 1u - i : 0u];
-      const uint32_t ra = rel[ka], rae = rel[ka + 1], rb = rel[kbi], rbe = rel[kbi + 1];
-      const uint32_t la = has_a ? rae - ra : 0u, lb = has_b ? rbe - rb : 0u;
-      const uint32_t kA = (la + 15u) >> 4, kB = (lb + 15u) >> 4;
-      const uint32_t pA = (0u - la) & 15u, pB = (0u - lb) & 15u;
-      const uint8_t* cpA = key0 + (int32_t)(rae - 16u * kA);
-      const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
-      const bool only_b = kA == 0;
-      uint64_t hw0, hw1;
-      pair_walk(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_spad, s_mask,
-                hw0, hw1);
-      const uint64_t hA = kA ? hw0 : 0, hB = kB ? (only_b ? hw0 : hw1) : 0;
-      if (has_a) {
-        h1[t0 + ka] = hA;
-        if constexpr (H2) h2[t0 + ka] = second_from_first(hA, la, key0 + rae);
-        if constexpr (EPI) bucket_emit<false>(bp, t0 + ka, hA);
-      }
-      if (has_b) {
-        h1[t0 + kbi] = hB;
-        if constexpr (H2) h2[t0 + kbi] = second_from_first(hB, lb, key0 + rbe);
-        if constexpr (EPI) bucket_emit<false>(bp, t0 + kbi, hB);
-      }
-    }
-    return;
-  }
-
-  if (wave == 4) {  // ---- sort wave: offsets, length classes, order, tile info ----
-    uint32_t pa[9];
-    uint64_t pz = 0, pe = 0;
-    // (per-lane vector loads through an index the compiler cannot see is zero: no scalar
-    // loads, whose out-of-order return would turn every LDS wait into lgkmcnt(0))
-    auto fetch = [&](uint64_t tile) {
-      const uint64_t t0 = tile * TK;
-      const uint32_t cnt = tile_cnt(t0);
-      uint32_t zero = 0;
-      asm volatile("" : "+v"(zero));
-#pragma unroll
-      for (uint32_t q = 0; q < 9; ++q) {
-        const uint32_t k = lane + 64u * q;
-        pa[q] = off32[2 * (t0 + (k < cnt ? k : cnt))];
-      }
-      pz = offsets[t0 + zero];
-      pe = offsets[t0 + cnt + zero];
-    };
-    if (J) fetch(first);
-    for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t b = j & 1u;
-      const uint64_t tile = first + (uint64_t)j * stride, t0 = tile * TK;
-      const uint32_t cnt = tile_cnt(t0);
-      const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
-      if (PROBE == 2 && j >= 2) {
-        lds_barrier();
-        continue;
-      }
-      uint32_t cur[9];
-#pragma unroll
-      for (uint32_t q = 0; q < 9; ++q) cur[q] = pa[q] - (uint32_t)o0;
-      if (j + 1 < J) fetch(tile + stride);
-      const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
-      const uint32_t delta = (uint32_t)(kb & 15u);
-      const uint64_t span = oN - o0 + delta;
-      if (span > kStage) {
-        if (lane == 0) {
-          over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
-          s_info[2 * b] = 0;
-        }
-      } else {
-        uint32_t* rel = s_rel + b * (TK + 1);
-        uint16_t* ord = s_order + b * TK;
-#pragma unroll
-        for (uint32_t q = 0; q < 9; ++q) {
-          const uint32_t k = lane + 64u * q;
-          if (k <= cnt) rel[k] = cur[q];
-        }
-        s_hist[lane] = 0;
-        s_hist[lane + 64] = 0;
-        uint32_t bins[8];
-#pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
-          const uint32_t k = lane + 64u * q;
-          // key k's end offset: the next lane's value (lane 63: lane 0 of the next row);
-          // taken with every lane active
-          const uint32_t nx = (uint32_t)__shfl_down((int)cur[q], 1, 64);
-          const uint32_t n0 = __builtin_amdgcn_readfirstlane(cur[q + 1]);
-          bins[q] = len_bin128_32((lane == 63 ? n0 : nx) - cur[q]);
-          if (k < cnt) lds_add(&s_hist[bins[q]], 1u);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint32_t v0 = s_hist[2 * lane], v1 = s_hist[2 * lane + 1], sum = v0 + v1;
-        uint32_t incl = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          uint32_t y = __shfl_up(incl, d, 64);
-          if (lane >= (uint32_t)d) incl += y;
-        }
-        s_hist[2 * lane] = incl - sum;
-        s_hist[2 * lane + 1] = incl - sum + v0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (uint32_t q = 0; q < 8; ++q) {
-          const uint32_t k = lane + 64u * q;
-          if (k < cnt) ord[lds_add_rtn(&s_hist[bins[q]], 1u)] = (uint16_t)k;
-        }
-        if (lane == 0) {
-          s_info[2 * b] = cnt;
-          s_info[2 * b + 1] = delta;
-        }
-      }
-      lds_barrier();  // slot b prepared (LDS writes complete); the hash waves start on it
-    }
-    return;
-  }
-
-  // ---- DMA waves: tile j's byte span into slot j&1's stage ----
-  {
-    const uint32_t dw = wave - 5u;
-    uint64_t pz = 0, pe = 0;
-    auto fetch = [&](uint64_t tile) {
-      const uint64_t t0 = tile * TK;
-      const uint32_t cnt = tile_cnt(t0);
-      uint32_t zero = 0;
-      asm volatile("" : "+v"(zero));
-      pz = offsets[t0 + zero];
-      pe = offsets[t0 + cnt + zero];
-    };
-    if (J) fetch(first);
-    for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t b = j & 1u;
-      const uint64_t tile = first + (uint64_t)j * stride;
-      const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
-      if (PROBE == 2 && j >= 2) {
-        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
-        continue;
-      }
-      if (j + 1 < J) fetch(tile + stride);
-      const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
-      const uint64_t span_lo = kb & ~15ull;
-      const uint64_t span = oN - o0 + (kb & 15u);
-      if (span <= kStage && oN > o0) {
-        // 1 KiB pieces, 16 B per lane; lanes past the span re-read its last 16 B into
-        // stage bytes nobody reads
-        const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
-        const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
-        const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
-        uint8_t* dst = s_stage + b * kSlot + 16;
-        uint32_t off = 1024u * dw + 16u * lane;
-        for (uint32_t c = dw; c < npieces; c += NDMA, off += 1024u * NDMA) {
-          const uint32_t o = off < lastp ? off : lastp;
-          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
-                                           (__attribute__((address_space(3))) void*)(dst + 1024u * c), 16, 0, 0);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");  // slot b's bytes have landed
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// CSR queue tiles (round 2).  One persistent 768-thread block per CU, two LDS tile slots
-// (stage, tile-relative offsets, length-sorted order) and waves split by role:
-//   waves 0-7   hash: each claims 64-key groups of the tile in its current slot (longest
-//               first) from an LDS counter, one key per lane, and moves on to the next
-//               tile when the slot has no group left -- two hash waves per SIMD at all
-//               times, the FNV chain of one wave alone being latency-bound (a single
-//               wave per SIMD ran the same tiles at ~290 ns per chunk step instead of
-//               ~165, fnv_csr_dbuf_kernel);
-//   wave 8      sort: tile offsets -> LDS, counting sort by chunk count, tile info;
-//   waves 9-11  DMA the tile's byte span into the slot's stage.
-// A slot is refilled once all eight hash waves have left the tile it held; the feeders
-// prefetch the next tile's offsets into registers, so offset loads, sort and DMA run
-// under the hash of the previous tile and no block-wide barrier is taken per tile.
-// Control words per slot (cumulative counters, never reset, except the claim counter,
-// which only the sort wave touches while no hash wave is in the slot):
-//   [0] ready: tile index + 1 of the tile the slot holds, [1] claims, [2] hash waves
-//   left, [3] feeder waves done, [4] key count (0 = not staged: ring list), [5] delta.
-// Tiles whose span exceeds the stage go to the ring list, as in lean2.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t lds_u32addr(const uint32_t* p) {
-  return (uint32_t)(uintptr_t)(__attribute__((address_space(3))) const uint32_t*)p;
-}
-// A control word read that waits for its value (polling / after a flag: no reordering).
-__device__ __forceinline__ uint32_t lds_poll(const uint32_t* p) {
-  uint32_t v;
-  asm volatile("ds_read_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(lds_u32addr(p)) : "memory");
-  return __builtin_amdgcn_readfirstlane(v);
-}
-__device__ __forceinline__ void lds_wait_ge(const uint32_t* p, uint32_t target) {
-  while (lds_poll(p) < target) __builtin_amdgcn_s_sleep(1);
-}
-
-// PROBE (lab timing probes, wrong hashes): 1 = hash waves claim groups without hashing,
-// 2 = feeders stage the first two tiles only (later tiles re-hash stale slots);
-// 3 (correct hashes) = feeder waves at raised issue priority.
-// TK_ keys per tile (a multiple of 64, <= 512), NSLOT tile slots of STAGE_KIB KiB.
-template <bool H2, bool EPI = false, int PROBE = 0, int TK_ = 512, int NSLOT = 2, int STAGE_KIB = 72>
-__global__ __launch_bounds__(768) void fnv_csr_queue_kernel(const uint8_t* __restrict__ bytes,
-                                                            const uint64_t* __restrict__ offsets, uint64_t n,
-                                                            SpadTable spad_tab, uint64_t* __restrict__ h1,
-                                                            uint64_t* __restrict__ h2, uint32_t* __restrict__ over_list,
-                                                            uint32_t* __restrict__ over_count, BucketParams bp = {}) {
-  constexpr uint32_t TK = TK_, NB = 128, NH = 8, NDMA = 3, NF = 1 + NDMA, NQ = TK / 64;
-  static_assert(TK % 64 == 0 && TK <= 512, "whole rows of 64 keys");
-  constexpr uint32_t kStage = STAGE_KIB * 1024u;
-  constexpr uint32_t kSlot = 16 + kStage + 1024u;  // + the overhang of the span's last 1 KiB DMA piece
-  __shared__ __attribute__((aligned(16))) uint8_t s_stage[NSLOT * kSlot];
-  __shared__ uint32_t s_rel[NSLOT * (TK + 1)];
-  __shared__ uint16_t s_order[NSLOT * TK];
-  __shared__ uint32_t s_ctl[8 * NSLOT];
-  __shared__ uint32_t s_hist[NB];
-  __shared__ uint64_t s_spad[16];
-  __shared__ uint4 s_mask[16];
-
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const uint64_t ntiles = (n + TK - 1) / TK;
-  const uint64_t first = blockIdx.x, stride = gridDim.x;
-  const uint32_t J = first < ntiles ? (uint32_t)((ntiles - first + stride - 1) / stride) : 0u;
-  if (tid < 16) {
-    s_spad[tid] = spad_tab.v[tid];
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {  // bytes >= p kept: chunk 0's p pad bytes zeroed
-      int32_t sh = 8 * ((int32_t)tid - 4 * i);
-      w[i] = sh <= 0 ? ~0u : sh >= 32 ? 0u : ~0u << sh;
-    }
-    s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
-    if (tid < 8 * NSLOT) s_ctl[tid] = 0;
-  }
-  if (tid >= 16 && tid < 8 * NSLOT) s_ctl[tid] = 0;
-  __syncthreads();
-  auto tile_cnt = [n](uint64_t t0) -> uint32_t { return (uint32_t)(n - t0 < (uint64_t)TK ? n - t0 : (uint64_t)TK); };
-  auto rfl64 = [](uint64_t v) -> uint64_t {
-    // (readfirstlane returns int: each half goes through uint32_t, or the low one sign-extends)
-    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-  };
-  // a feeder wave's part of tile j is in LDS: count it; the last of the NF publishes the slot
-  auto feeder_done = [&](uint32_t j) {
-    uint32_t* ctl = s_ctl + 8u * (j % NSLOT);
-    uint32_t old = 0;
-    if (lane == 0) old = lds_add_rtn(&ctl[3], 1u);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old == NF * (j / NSLOT + 1u) - 1u && lane == 0)
-      asm volatile("ds_write_b32 %0, %1\n\ts_waitcnt lgkmcnt(0)" ::"v"(lds_u32addr(&ctl[0])), "v"(j + 1u) : "memory");
-  };
-  const uint32_t* off32 = reinterpret_cast<const uint32_t*>(offsets);
-
-  if (wave < NH) {  // ---- hash waves ----
-    for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t b = j % NSLOT;
-      uint32_t* ctl = s_ctl + 8u * b;
-      lds_wait_ge(&ctl[0], j + 1u);
-      const uint32_t cnt = lds_poll(&ctl[4]);
-      const uint32_t delta = lds_poll(&ctl[5]);
-      const uint32_t ngroups = (cnt + 63u) >> 6;
-      const uint64_t t0 = (first + (uint64_t)j * stride) * TK;
-      const uint16_t* ord = s_order + b * TK;
-      const uint32_t* rel = s_rel + b * (TK + 1);
-      const uint8_t* key0 = s_stage + b * kSlot + 16 + delta;
-      for (;;) {
-        uint32_t c = 0;
-        if (lane == 0) c = lds_add_rtn(&ctl[1], 1u);
-        c = __builtin_amdgcn_readfirstlane(c);
-        if (c >= ngroups) break;
-        if constexpr (PROBE == 1) continue;
-        const uint32_t idx = 64u * (ngroups - 1u - c) + lane;  // longest groups first
-        const bool valid = idx < cnt;
-        const uint32_t k = ord[valid ? idx : cnt - 1u];
-        uint64_t r1, r2;
-        lds_hash32<false>(valid, rel[k], rel[k + 1], key0, s_spad, s_mask, r1, r2);
-        if (valid) {
-          h1[t0 + k] = r1;
-          if constexpr (H2) h2[t0 + k] = r2;
-          if constexpr (EPI) bucket_emit<false>(bp, t0 + k, r1);
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every read of the slot has returned
-      if (lane == 0) lds_add(&ctl[2], 1u);                 // this wave has left the slot
-    }
-    return;
-  }
-
-  // the feeders issue ahead of the hash waves sharing their SIMD (PROBE 3)
-  if constexpr (PROBE == 3) __builtin_amdgcn_s_setprio(3);
-  if (wave == NH) {  // ---- sort wave: offsets, length classes, order, tile info ----
-    uint32_t pa[NQ + 1];
-    uint64_t pz = 0, pe = 0;
-    // (per-lane vector loads through an index the compiler cannot see is zero: no scalar
-    // loads, whose out-of-order return would turn every LDS wait into lgkmcnt(0))
-    auto fetch = [&](uint64_t tile) {
-      const uint64_t t0 = tile * TK;
-      const uint32_t cnt = tile_cnt(t0);
-      uint32_t zero = 0;
-      asm volatile("" : "+v"(zero));
-#pragma unroll
-      for (uint32_t q = 0; q < NQ + 1; ++q) {
-        const uint32_t k = lane + 64u * q;
-        pa[q] = off32[2 * (t0 + (k < cnt ? k : cnt) + zero)];
-      }
-      pz = offsets[t0 + zero];
-      pe = offsets[t0 + cnt + zero];
-    };
-    if (J) fetch(first);
-    for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t b = j % NSLOT;
-      uint32_t* ctl = s_ctl + 8u * b;
-      const uint64_t tile = first + (uint64_t)j * stride, t0 = tile * TK;
-      const uint32_t cnt = tile_cnt(t0);
-      const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
-      uint32_t cur[NQ + 1];
-#pragma unroll
-      for (uint32_t q = 0; q < NQ + 1; ++q) cur[q] = pa[q] - (uint32_t)o0;
-      if (j + 1 < J) fetch(tile + stride);
-      const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
-      const uint32_t delta = (uint32_t)(kb & 15u);
-      const uint64_t span = oN - o0 + delta;
-      lds_wait_ge(&ctl[2], NH * (j / NSLOT));  // every hash wave has left the slot's previous tile
-      if (PROBE == 2 && j >= NSLOT) {
-        if (lane == 0) ctl[1] = 0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        feeder_done(j);
-        continue;
-      }
-      uint32_t* rel = s_rel + b * (TK + 1);
-      uint16_t* ord = s_order + b * TK;
-      const bool staged = span <= kStage;
-      if (!staged) {
-        if (lane == 0) over_list[atomicAdd(over_count, 1u)] = (uint32_t)tile;
-      } else {
-#pragma unroll
-        for (uint32_t q = 0; q < NQ + 1; ++q) {
-          const uint32_t k = lane + 64u * q;
-          if (k <= cnt) rel[k] = cur[q];
-        }
-        s_hist[lane] = 0;
-        s_hist[lane + 64] = 0;
-        uint32_t bins[NQ];
-#pragma unroll
-        for (uint32_t q = 0; q < NQ; ++q) {
-          const uint32_t k = lane + 64u * q;
-          // key k's end offset: the next lane's value (lane 63: lane 0 of the next row);
-          // taken with every lane active
-          const uint32_t nx = (uint32_t)__shfl_down((int)cur[q], 1, 64);
-          const uint32_t n0 = __builtin_amdgcn_readfirstlane(cur[q + 1]);
-          bins[q] = len_bin128_32((lane == 63 ? n0 : nx) - cur[q]);
-          if (k < cnt) lds_add(&s_hist[bins[q]], 1u);
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint32_t v0 = s_hist[2 * lane], v1 = s_hist[2 * lane + 1], sum = v0 + v1;
-        uint32_t incl = sum;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          uint32_t y = __shfl_up(incl, d, 64);
-          if (lane >= (uint32_t)d) incl += y;
-        }
-        s_hist[2 * lane] = incl - sum;
-        s_hist[2 * lane + 1] = incl - sum + v0;
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-        for (uint32_t q = 0; q < NQ; ++q) {
-          const uint32_t k = lane + 64u * q;
-          if (k < cnt) ord[lds_add_rtn(&s_hist[bins[q]], 1u)] = (uint16_t)k;
-        }
-      }
-      if (lane == 0) {
-        ctl[1] = 0;  // claims (no hash wave is in the slot)
-        ctl[4] = staged ? cnt : 0u;
-        ctl[5] = delta;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      feeder_done(j);
-    }
-    return;
-  }
-
-  // ---- DMA waves: tile j's byte span into slot j&1's stage ----
-  {
-    const uint32_t dw = wave - (NH + 1u);
-    uint64_t pz = 0, pe = 0;
-    auto fetch = [&](uint64_t tile) {
-      const uint64_t t0 = tile * TK;
-      const uint32_t cnt = tile_cnt(t0);
-      uint32_t zero = 0;
-      asm volatile("" : "+v"(zero));
-      pz = offsets[t0 + zero];
-      pe = offsets[t0 + cnt + zero];
-    };
-    if (J) fetch(first);
-    for (uint32_t j = 0; j < J; ++j) {
-      const uint32_t b = j % NSLOT;
-      const uint64_t tile = first + (uint64_t)j * stride;
-      const uint64_t o0 = rfl64(pz), oN = rfl64(pe);
-      if (j + 1 < J) fetch(tile + stride);
-      const uint64_t kb = (uint64_t)(uintptr_t)bytes + o0;
-      const uint64_t span_lo = kb & ~15ull;
-      const uint64_t span = oN - o0 + (kb & 15u);
-      lds_wait_ge(&s_ctl[8u * b + 2u], NH * (j / NSLOT));  // the slot's previous tile is consumed
-      if (span <= kStage && oN > o0 && !(PROBE == 2 && j >= NSLOT)) {
-        // 1 KiB pieces, 16 B per lane; lanes past the span re-read its last 16 B into
-        // stage bytes nobody reads
-        const uint32_t npieces = (uint32_t)((span + 1023) >> 10);
-        const uint32_t lastp = ((uint32_t)span - 1u) & ~15u;
-        const uint8_t* src0 = (const uint8_t*)(uintptr_t)span_lo;
-        uint8_t* dst = s_stage + b * kSlot + 16;
-        uint32_t off = 1024u * dw + 16u * lane;
-        for (uint32_t c = dw; c < npieces; c += NDMA, off += 1024u * NDMA) {
-          const uint32_t o = off < lastp ? off : lastp;
-          __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src0 + o),
-                                           (__attribute__((address_space(3))) void*)(dst + 1024u * c), 16, 0, 0);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's pieces have landed
-      feeder_done(j);
     }
   }
 }
@@ -2190,183 +1253,9 @@ static hipError_t launch_lean2(const uint8_t* b, const uint64_t* offsets, uint64
   return hipGetLastError();
 }
 
-// Resident blocks of kernel K per device (occupancy x CUs), computed once per device and
-// kernel (the cache is per template instance, i.e. per kernel); safe from any thread.
-template <auto K>
-static unsigned resident_grid(int threads, unsigned cap) {
-  constexpr int kMaxDev = 64;
-  static std::atomic<unsigned> cache[kMaxDev];
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) dev = 0;
-  unsigned g = cache[dev].load(std::memory_order_relaxed);
-  if (!g) {
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)K, threads, 0) != hipSuccess || per_cu <= 0)
-      per_cu = 1;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-    g = (unsigned)(per_cu * cus);
-    cache[dev].store(g, std::memory_order_relaxed);
-  }
-  return g < cap ? g : cap;
-}
-
-// pair-tile kernel (TK = 128 NW keys) + the ring pass over its oversize-tile list
-template <int NW, int KIB, bool PERSIST, bool STAGGER = false, bool W2 = false, bool Z = false>
-static hipError_t launch_pair(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
-                              uint64_t* h2, const BucketParams* bp, hipStream_t stream) {
-  constexpr uint64_t TK = 128 * NW;
-  const uint64_t ntiles = (n + TK - 1) / TK;
-  if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  uint32_t* scratch = nullptr;  // [0] = count, [1..] = tile list
-  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (ntiles + 1), stream);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(scratch, 0, 4, stream);
-  const BucketParams none{};
-  const BucketParams& p = bp ? *bp : none;
-  const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
-#define K2H_PAIR(H2, EPI)                                                                                        \
-  {                                                                                                            \
-    constexpr auto k = fnv_csr_pair_kernel<H2, EPI, NW, KIB, PERSIST, STAGGER, W2, Z>;                            \
-    const unsigned g = PERSIST ? resident_grid<k>(NW * 64, (unsigned)ntiles) : (unsigned)ntiles;               \
-    k<<<g, NW * 64, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, scratch + 1, scratch, p);            \
-    fnv_csr_ring_list_kernel<H2, EPI, (int)TK><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, \
-                                                                       scratch + 1, scratch, p);               \
-  }
-  if (e == hipSuccess) {
-    if (bp) {
-      if (h2) K2H_PAIR(true, true) else K2H_PAIR(false, true)
-    } else {
-      if (h2) K2H_PAIR(true, false) else K2H_PAIR(false, false)
-    }
-    e = hipGetLastError();
-  }
-#undef K2H_PAIR
-  hipError_t f = hipFreeAsync(scratch, stream);
-  return e != hipSuccess ? e : f;
-}
-
-// Double-buffered tile kernel (one persistent block per CU) + the ring pass over its
-// oversize-tile list.
-template <int PROBE = 0, bool QUEUE = false>
-[[maybe_unused]] static hipError_t launch_dbuf(const uint8_t* b, const uint64_t* offsets, uint64_t n, const SpadTable& t, uint64_t* h1,
-                              uint64_t* h2, const BucketParams* bp, hipStream_t stream) {
-  constexpr uint64_t TK = 512;
-  const uint64_t ntiles = (n + TK - 1) / TK;
-  if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  uint32_t* scratch = nullptr;  // [0] = count, [1..] = tile list
-  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (ntiles + 1), stream);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(scratch, 0, 4, stream);
-  const BucketParams none{};
-  const BucketParams& p = bp ? *bp : none;
-  const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
-#define K2H_DBUF(H2, EPI)                                                                                        \
-  {                                                                                                            \
-    constexpr auto k = QUEUE ? fnv_csr_queue_kernel<H2, EPI, PROBE> : fnv_csr_dbuf_kernel<H2, EPI, PROBE>;               \
-    constexpr int nt = QUEUE ? 768 : 512;                                                                      \
-    const unsigned g = resident_grid<k>(nt, (unsigned)ntiles);                                                 \
-    k<<<g, nt, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, scratch + 1, scratch, p);                 \
-    fnv_csr_ring_list_kernel<H2, EPI, (int)TK><<<gl, 256, 0, stream>>>(b, offsets, n, t, h1, H2 ? h2 : nullptr, \
-                                                                       scratch + 1, scratch, p);               \
-  }
-  if (e == hipSuccess) {
-    if (bp) {
-      if (h2) K2H_DBUF(true, true) else K2H_DBUF(false, true)
-    } else {
-      if (h2) K2H_DBUF(true, false) else K2H_DBUF(false, false)
-    }
-    e = hipGetLastError();
-  }
-#undef K2H_DBUF
-  hipError_t f = hipFreeAsync(scratch, stream);
-  return e != hipSuccess ? e : f;
-}
-
-// lean2 with its load / sort phase at issue priority PRIO (lab A/B)
-template <int PRIO, bool SCAN1 = false, bool WALK4 = false, int DESYNC = 0>
-[[maybe_unused]] static hipError_t launch_lean2_prio(const uint8_t* bb, const uint64_t* offsets, uint64_t n,
-                                                     const SpadTable& t, uint64_t* h1, uint64_t* h2, hipStream_t stream) {
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
-  const uint64_t C = (uint64_t)cus;
-  // halves: C half tiles (desync 1) or C half + C full in the first 2C blocks (desync 2)
-  const uint64_t lead = DESYNC == 1 ? C * (kTileKeys / 2) : DESYNC == 2 ? C * (kTileKeys + kTileKeys / 2) : 0;
-  const uint64_t nlead = DESYNC == 1 ? C : DESYNC == 2 ? 2 * C : 0;
-  if (DESYNC && n <= lead) return hipErrorInvalidValue;  // lab: large inputs only
-  const unsigned g = DESYNC ? (unsigned)(nlead + (n - lead + kTileKeys - 1) / kTileKeys) : (unsigned)((n + kTileKeys - 1) / kTileKeys);
-  const unsigned gl = g < 512u ? g : 512u;
-  uint32_t* scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (g + 1), stream);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(scratch, 0, 4, stream);
-  if (e == hipSuccess) {
-    if (h2) {
-      fnv_csr_lean2_kernel<true, false, 3, false, PRIO, SCAN1, WALK4, DESYNC><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch, BucketParams{}, (uint32_t)cus);
-      fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
-    } else {
-      fnv_csr_lean2_kernel<false, false, 3, false, PRIO, SCAN1, WALK4, DESYNC><<<g, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch, BucketParams{}, (uint32_t)cus);
-      fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
-    }
-    e = hipGetLastError();
-  }
-  hipError_t f = hipFreeAsync(scratch, stream);
-  return e != hipSuccess ? e : f;
-}
-
-// persistent lean3 (lab A/B)
-[[maybe_unused]] static hipError_t launch_lean3(const uint8_t* bb, const uint64_t* offsets, uint64_t n, const SpadTable& t,
-                                                uint64_t* h1, uint64_t* h2, hipStream_t stream) {
-  const uint64_t ntiles = (n + kTileKeys - 1) / kTileKeys;
-  if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
-  uint32_t* scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (ntiles + 1), stream);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(scratch, 0, 4, stream);
-  if (e == hipSuccess) {
-    if (h2) {
-      constexpr auto k = fnv_csr_lean3_kernel<true>;
-      k<<<resident_grid<k>(256, (unsigned)ntiles), 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch, BucketParams{});
-      fnv_csr_ring_list_kernel<true><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
-    } else {
-      constexpr auto k = fnv_csr_lean3_kernel<false>;
-      k<<<resident_grid<k>(256, (unsigned)ntiles), 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch, BucketParams{});
-      fnv_csr_ring_list_kernel<false><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
-    }
-    e = hipGetLastError();
-  }
-  hipError_t f = hipFreeAsync(scratch, stream);
-  return e != hipSuccess ? e : f;
-}
-
-// queue tiles of 320 keys in three 46 KiB slots, feeders at raised priority (lab A/B)
-[[maybe_unused]] static hipError_t launch_queue320(const uint8_t* bb, const uint64_t* offsets, uint64_t n, const SpadTable& t,
-                                                   uint64_t* h1, uint64_t* h2, hipStream_t stream) {
-  constexpr uint64_t TK = 320;
-  const uint64_t ntiles = (n + TK - 1) / TK;
-  if (ntiles > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  const unsigned gl = ntiles < 512u ? (unsigned)ntiles : 512u;
-  uint32_t* scratch = nullptr;
-  hipError_t e = hipMallocAsync((void**)&scratch, 4ull * (ntiles + 1), stream);
-  if (e != hipSuccess) return e;
-  e = hipMemsetAsync(scratch, 0, 4, stream);
-  if (e == hipSuccess) {
-    if (h2) {
-      constexpr auto k = fnv_csr_queue_kernel<true, false, 3, 320, 3, 46>;
-      k<<<resident_grid<k>(768, (unsigned)ntiles), 768, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch, BucketParams{});
-      fnv_csr_ring_list_kernel<true, false, 320><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, h2, scratch + 1, scratch);
-    } else {
-      constexpr auto k = fnv_csr_queue_kernel<false, false, 3, 320, 3, 46>;
-      k<<<resident_grid<k>(768, (unsigned)ntiles), 768, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch, BucketParams{});
-      fnv_csr_ring_list_kernel<false, false, 320><<<gl, 256, 0, stream>>>(bb, offsets, n, t, h1, nullptr, scratch + 1, scratch);
-    }
-    e = hipGetLastError();
-  }
-  hipError_t f = hipFreeAsync(scratch, stream);
-  return e != hipSuccess ? e : f;
-}
-
 #if K2H_AMD_LAB
+#include "k2h_csr_lab.inc"
+
 static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                            uint64_t* h2, int mode, hipStream_t stream, const BucketParams* bp) {
   SpadTable t = make_spad(seed);
