@@ -42,6 +42,24 @@ def test_header_symbols_exported():
         assert hasattr(plug, s)
 
 
+# Kernels that exist only as measured A/B variants (the lab build, tools/lab/); none may be
+# compiled into the product library.
+LAB_ONLY_KERNELS = ("fnv_csr_dbuf_kernel", "fnv_csr_queue_kernel", "fnv_csr_lean3_kernel", "fnv_csr_pair_kernel",
+                    "fnv_csr_lean_kernel", "fnv_csr_tile_kernel", "fnv_csr_simple_kernel", "fnv_fixed32_pipe_kernel",
+                    "fnv_fixed32_ring_kernel", "ralledata_group_kernel", "ralledata_stage_kernel",
+                    "ralledata_batch_kernel")
+
+
+def test_product_library_has_no_lab_code():
+    blob = Path(_native.BATCH_LIB).read_bytes()
+    for name in LAB_ONLY_KERNELS:
+        assert name.encode() not in blob, name
+    lib = ctypes.CDLL(str(_native.BATCH_LIB))
+    assert not hasattr(lib, "k2h_amd_set_variant") and not hasattr(lib, "k2h_amd_get_variant")
+    # the product CSR path is the lean2 tile kernel plus the ring pass for oversize tiles
+    assert b"fnv_csr_lean2_kernel" in blob and b"fnv_csr_ring_list_kernel" in blob
+
+
 def test_plugin_has_no_hip_dependency():
     out = subprocess.run(["ldd", str(_native.PLUGIN_LIB)], capture_output=True, text=True).stdout
     assert "amdhip" not in out and "hsa" not in out
