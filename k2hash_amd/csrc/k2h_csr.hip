@@ -331,7 +331,7 @@ enum {
   kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
   kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
   kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30,
-  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36, kModeLean2Desync1 = 37, kModeLean2Desync2 = 38, kModeQueue320 = 39
+  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36, kModeLean2Desync1 = 37, kModeLean2Desync2 = 38, kModeQueue320 = 39, kModeLean2PrioSetup = 40
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
     clk0 = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+  if constexpr (PRIO) __builtin_amdgcn_s_setprio(PRIO == 4 ? 1 : PRIO);  // 4 (lab): 1, dropped at the walk
   const uint32_t tid = threadIdx.x, lane = tid & 63u;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   // DESYNC (lab; ncu = CU count): some blocks of the first wave take half tiles, so the two
@@ -996,7 +996,7 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
   __syncthreads();                                   // ... and every other wave's
 
   const uint8_t* key0 = s_stage + 16 + delta;
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(0);
+  if constexpr (PRIO && PRIO != 4) __builtin_amdgcn_s_setprio(0);
   if constexpr (WALK == 3) {
     // Pair walk: lane i (0..255) takes sorted keys i and cnt-1-i, a short and a long one,
     // and hashes them back to back; sums of the pair lengths are nearly equal across a
@@ -1013,6 +1013,7 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
     const uint8_t* cpB = key0 + (int32_t)(rbe - 16u * kB);
     const bool only_b = kA == 0;  // key A empty (or absent): walk B alone
     uint64_t hw0, hw1;
+    if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(0);
 #if K2H_AMD_LAB
     if constexpr (WALK4)
       pair_walk3(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
@@ -1265,6 +1266,7 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeLean2Prio) return launch_lean2_prio<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio3) return launch_lean2_prio<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2PrioSetup) return launch_lean2_prio<4, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeQueue320) return launch_queue320((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Desync1) return launch_lean2_prio<1, true, false, 1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Desync2) return launch_lean2_prio<1, true, false, 2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);

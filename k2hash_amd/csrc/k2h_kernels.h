@@ -121,6 +121,7 @@ enum {
   kVariantCsrLean2Desync1 = 98,   // csr lean2 (product settings), first-wave half tiles so co-resident tiles start out
   kVariantCsrLean2Desync2 = 99,   // of phase (98: blocks [0, #CU); 99: even blocks of [0, 2 #CU))
   kVariantCsrQueue320 = 100,      // csr queue tiles of 320 keys in three 46 KiB slots, feeders at raised priority
+  kVariantCsrLean2PrioSetup = 101, // csr lean2 (one-wave scan) with priority 1 kept through the pair setup, dropped at the walk
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };

@@ -848,6 +848,7 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrLean2Desync1 ? 37
                          : variant == kVariantCsrLean2Desync2 ? 38
                          : variant == kVariantCsrQueue320 ? 39
+                         : variant == kVariantCsrLean2PrioSetup ? 40
                          : variant == kVariantCsrQueueProbeNoHash ? 28
                          : variant == kVariantCsrQueueProbeNoFeed ? 29
                          : variant == kVariantCsrDbufProbeNoHash ? 25
