@@ -331,7 +331,7 @@ enum {
   kModePair2 = 15, kModePair2P = 16, kModePair4P = 17, kModePair4 = 18, kModePair4PS = 19, kModePair2PS = 20, kModePair4W2 = 21, kModePair4Z = 22, kModeLean2Clock = 23,
   kModeDbuf = 24, kModeDbufProbeNoHash = 25, kModeDbufProbeNoFeed = 26, kModeQueue = 27,
   kModeQueueProbeNoHash = 28, kModeQueueProbeNoFeed = 29, kModeQueuePrio = 30,
-  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36, kModeLean2Desync1 = 37, kModeLean2Desync2 = 38, kModeQueue320 = 39, kModeLean2PrioSetup = 40
+  kModeLean2Prio = 31, kModeLean2Prio3 = 32, kModeLean2Prio1 = 33, kModeLean2Scan1 = 34, kModeLean2Runs = 35, kModeLean3 = 36, kModeLean2Desync1 = 37, kModeLean2Desync2 = 38, kModeQueue320 = 39, kModeLean2PrioSetup = 40, kModeLean2Ballot = 41
 };
 
 // Phase stamps of the profiling mode (kModeStagedProf; tools/csr_phases.py): 100 MHz
@@ -873,7 +873,7 @@ __device__ __forceinline__ void pair_walk2(uint32_t k0, uint32_t p0, const uint8
 // raised issue priority, back to normal for the hash walk, so a tile's setup is not queued
 // behind the other block's hash instructions on the same SIMD.
 // SCAN1 (lab): the 128-class scan by wave 0 alone, two classes per lane (one barrier fewer).
-template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0, bool SCAN1 = false, bool WALK4 = false,
+template <bool H2, bool EPI = false, int WALK = 0, bool CLK = false, int PRIO = 0, bool SCAN1 = false, int WALK4 = 0,
           int DESYNC = 0>
 __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __restrict__ bytes,
                                                             const uint64_t* __restrict__ offsets, uint64_t n,
@@ -1015,8 +1015,11 @@ __global__ __launch_bounds__(256) void fnv_csr_lean2_kernel(const uint8_t* __res
     uint64_t hw0, hw1;
     if constexpr (PRIO == 4) __builtin_amdgcn_s_setprio(0);
 #if K2H_AMD_LAB
-    if constexpr (WALK4)
+    if constexpr (WALK4 == 1)
       pair_walk3(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
+                 s_spad, s_mask, hw0, hw1);
+    else if constexpr (WALK4 == 2)
+      pair_walk4(only_b ? kB : kA, only_b ? pB : pA, only_b ? cpB : cpA, only_b ? 0u : kB, pB, cpB, s_stage + 16,
                  s_spad, s_mask, hw0, hw1);
     else
 #endif
@@ -1266,12 +1269,13 @@ static hipError_t launch_csr_tile_lab(const void* bytes, const uint64_t* offsets
   if (mode == kModeQueueProbeNoFeed) return launch_dbuf<2, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);
   if (mode == kModeLean2Prio) return launch_lean2_prio<2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio3) return launch_lean2_prio<3>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2Ballot) return launch_lean2_prio<1, true, 2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2PrioSetup) return launch_lean2_prio<4, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeQueue320) return launch_queue320((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Desync1) return launch_lean2_prio<1, true, false, 1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Desync2) return launch_lean2_prio<1, true, false, 2>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean3) return launch_lean3((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
-  if (mode == kModeLean2Runs) return launch_lean2_prio<1, true, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
+  if (mode == kModeLean2Runs) return launch_lean2_prio<1, true, 1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Scan1) return launch_lean2_prio<1, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeLean2Prio1) return launch_lean2_prio<1>((const uint8_t*)bytes, offsets, n, t, h1, h2, stream);
   if (mode == kModeQueuePrio) return launch_dbuf<3, true>((const uint8_t*)bytes, offsets, n, t, h1, h2, bp, stream);

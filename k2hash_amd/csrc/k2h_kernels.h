@@ -122,6 +122,7 @@ enum {
   kVariantCsrLean2Desync2 = 99,   // of phase (98: blocks [0, #CU); 99: even blocks of [0, 2 #CU))
   kVariantCsrQueue320 = 100,      // csr queue tiles of 320 keys in three 46 KiB slots, feeders at raised priority
   kVariantCsrLean2PrioSetup = 101, // csr lean2 (one-wave scan) with priority 1 kept through the pair setup, dropped at the walk
+  kVariantCsrLean2Ballot = 102,   // csr lean2 with the uniform-trip, ballot-guarded pair walk (pair_walk4)
   kVariantCsrPair4W2 = 68,        // csr pair tiles (512 keys) with the uniform-trip walk (pair_walk2)
   kVariantRalleStage = 65,        // ralledata: blobs of 64 records assembled in LDS, aligned line stores (slower)
 };

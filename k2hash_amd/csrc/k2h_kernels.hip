@@ -849,6 +849,7 @@ static hipError_t launch_csr_lab(const void* bytes, const uint64_t* offsets, uin
                          : variant == kVariantCsrLean2Desync2 ? 38
                          : variant == kVariantCsrQueue320 ? 39
                          : variant == kVariantCsrLean2PrioSetup ? 40
+                         : variant == kVariantCsrLean2Ballot ? 41
                          : variant == kVariantCsrQueueProbeNoHash ? 28
                          : variant == kVariantCsrQueueProbeNoFeed ? 29
                          : variant == kVariantCsrDbufProbeNoHash ? 25
