@@ -92,11 +92,17 @@ def test_golden_vectors_csr(cuda, vectors):
             assert (int(a[i]), int(b[i])) == (u64(v["h1"]), u64(v["h2"])), (field, v["tag"], v["len"])
 
 
-@pytest.mark.parametrize("lens", ["mixed", "zeros", "long", "uniform"])
+@pytest.mark.parametrize("lens", ["mixed", "zeros", "long", "uniform", "mixedtiles"])
 def test_csr_vs_oracle(cuda, oracle, lens):
     import torch
     rng = np.random.default_rng(5)
-    if lens == "mixed":
+    if lens == "mixedtiles":
+        # 512-key tiles alternating between LDS-staged (short keys) and oversize (spans past
+        # the 72 KiB stage: listed and hashed by the ring pass) in one call, last tile partial
+        L = rng.integers(8, 129, 512 * 7 + 77)
+        for t in (1, 4, 7):
+            L[512 * t: 512 * (t + 1)] = rng.integers(150, 400, L[512 * t: 512 * (t + 1)].size)
+    elif lens == "mixed":
         L = rng.integers(0, 300, 6000)
         L[rng.integers(0, 6000, 300)] = 0
     elif lens == "zeros":
