@@ -164,6 +164,30 @@ def test_fused_csr_vs_oracle(cuda, oracle):
 
 
 @pytest.mark.gpu
+def test_fused_csr_oversize_tiles_vs_oracle(cuda, oracle):
+    """The fused epilogue on both CSR paths in one call: LDS-staged tiles and tiles whose
+    span exceeds the stage (hashed by the ring pass with the epilogue fused there too),
+    with h2 and both index outputs."""
+    import torch
+    rng = np.random.default_rng(12)
+    L = rng.integers(0, 129, 512 * 5 + 33)
+    for t in (0, 3):
+        L[512 * t: 512 * (t + 1)] = rng.integers(160, 420, 512)
+    off = np.zeros(L.size + 1, np.int64)
+    off[1:] = np.cumsum(L)
+    data = oracle.gen_bytes(int(off[-1]) + 3)
+    r1, r2 = oracle.hash_csr(data, off.astype(np.uint64))
+    h1, h2, k, c = k2hash_amd.hash_csr_index(torch.from_numpy(data).to(cuda), torch.from_numpy(off).to(cuda),
+                                             (1 << 20) - 1, 0x7, second=True)
+    torch.cuda.synchronize()
+    rk, rc = oracle.bucket_index(r1, (1 << 20) - 1, 0x7)
+    assert np.array_equal(h1.cpu().numpy().view(np.uint64), r1)
+    assert np.array_equal(h2.cpu().numpy().view(np.uint64), r2)
+    assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
+    assert np.array_equal(c.cpu().numpy().view(np.uint64), rc)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("cfgname,cur,cm", [("fixed32_16M", 0xFF, 0xF), ("fixed32_16M", (1 << 28) - 1, 0xF),
                                              ("csr_8_256_64M", (1 << 24) - 1, 0x3F)])
 def test_fused_full_size_vs_oracle(cuda, oracle, digests, cfgname, cur, cm):
