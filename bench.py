@@ -83,7 +83,13 @@ def parse(argv=None):
                    help="no GPU: run the launcher / shard / gather path on CPU with the scalar plugin "
                         "(a rehearsal of the N>1 plumbing, not a measurement)")
     p.add_argument("--keys", type=int, default=0, help="override keys per rank (tests / rehearsals)")
-    p.add_argument("--child-timeout", type=float, default=1500.0)
+    p.add_argument("--child-timeout", type=float, default=540.0,
+                   help="self-launcher: kill every rank after this long (below the driver's 600 s limit)")
+    p.add_argument("--init-timeout", type=float, default=180.0,
+                   help="torch.distributed init / collective timeout in seconds (N > 1)")
+    p.add_argument("--inject-rank-failure", type=int, default=-1,
+                   help="TEST ONLY: this rank exits with status 3 right after joining the process group "
+                        "(exercises the launcher's fail-fast path)")
     return p.parse_args(argv)
 
 
@@ -101,25 +107,54 @@ def _free_port() -> int:
 def launch(args) -> int:
     """Start args.gpus ranks of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*),
     relay rank 0's stdout, return the worst exit code.  Runs before anything touches a
-    GPU; the children are new processes."""
+    GPU; the children are new processes (never an exec of this one).
+
+    Fail-fast: every child is polled; the first rank that exits non-zero (or a run past
+    --child-timeout) terminates the others, so a rank that dies in init or a collective
+    ends the run with an error instead of leaving rank 0 blocked in RCCL until the
+    driver's limit."""
+    import tempfile
+
     port = _free_port()
     procs = []
+    out0 = tempfile.TemporaryFile()  # rank 0's stdout (a file: no pipe to fill while we poll)
     for r in range(args.gpus):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
                    LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env,
-                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out, _ = procs[0].communicate(timeout=args.child_timeout)
-    rcs = [procs[0].returncode]
-    for p in procs[1:]:
-        try:
-            rcs.append(p.wait(timeout=60))
-        except subprocess.TimeoutExpired:
-            p.kill()
-            rcs.append(p.wait())
-    sys.stdout.write(out.decode())
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL))
+    print(f"launcher: rank pids {[p.pid for p in procs]}", file=sys.stderr, flush=True)
+    deadline = time.monotonic() + args.child_timeout
+    failed = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [(r, rc) for r, rc in enumerate(rcs) if rc not in (None, 0)]
+        if bad:
+            failed = f"rank {bad[0][0]} exited with {bad[0][1]}"
+            break
+        if all(rc == 0 for rc in rcs):
+            break
+        if time.monotonic() > deadline:
+            failed = f"ranks still running after --child-timeout {args.child_timeout:.0f} s"
+            break
+        time.sleep(0.05)
+    if failed:
+        print(f"launcher: {failed}; terminating the other ranks", file=sys.stderr, flush=True)
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    out0.seek(0)
+    sys.stdout.write(out0.read().decode(errors="replace"))
     sys.stdout.flush()
-    return max(abs(rc) for rc in rcs)
+    if failed:
+        return 1
+    return max(abs(p.returncode) for p in procs)
 
 
 # --------------------------------------------------------------------------------------
@@ -303,15 +338,31 @@ def timed(step, steps: int, warmup: int, warm_ms: float, world: int = 1, dist=No
     return elapsed, e0.elapsed_time(e1) / steps / 1e3, extra
 
 
-def valu_fields(name: str, kern_s: float, model_insts: float) -> dict:
+def _profile(kind: str, name: str, keys: int | None):
+    """profiles/<kind>_<name>.json scaled to a launch of `keys` keys: the counts are per
+    launch of the kernel over `keys_per_launch` keys, and every per-key quantity of these
+    kernels (instructions, bytes) is linear in the key count.  None when the profile is
+    missing or was not taken per key."""
+    prof = ROOT / "profiles" / f"{kind}_{name}.json"
+    if not prof.exists():
+        return None, None
+    d = json.loads(prof.read_text())
+    per = d.get("keys_per_launch")
+    if not per or not keys:
+        return None, None
+    return d, keys / per
+
+
+def valu_fields(name: str, kern_s: float, model_insts: float, keys: int | None = None) -> dict:
     """VALU-issue roofline: wave64 VALU instructions per launch (rocprofv3 SQ_INSTS_VALU pass,
-    profiles/valu_<name>.json, else the FNV-step model) at the peak issue rate, over the
-    measured launch time."""
+    profiles/valu_<name>.json scaled to this launch's key count, else the FNV-step model) at
+    the peak issue rate, over the measured launch time."""
     insts, src, clock = model_insts, "model: 86 slow-issue VALU ops per 16-byte chunk per 64 keys", None
-    prof = ROOT / "profiles" / f"valu_{name}.json"
-    if prof.exists():
-        d = json.loads(prof.read_text())
-        insts, src = float(d["valu_insts_per_launch"]), f"profiles/valu_{name}.json ({d.get('round', '')})"
+    d, scale = _profile("valu", name, keys)
+    if d is not None:
+        insts = float(d["valu_insts_per_launch"]) * scale
+        src = (f"profiles/valu_{name}.json ({d.get('round', '')}; {d['keys_per_launch']} keys per profiled launch, "
+               f"scaled x{scale:.4g} to this launch)")
     probe = ROOT / "profiles" / "clock_probe.json"  # tools/clock_probe.py: s_memtime / s_memrealtime per wave
     if probe.exists():
         clock = json.loads(probe.read_text()).get(name, {}).get("clock_ghz")
@@ -324,16 +375,19 @@ def valu_fields(name: str, kern_s: float, model_insts: float) -> dict:
     return r
 
 
-def traffic_of(name: str):
-    prof = ROOT / "profiles" / f"traffic_{name}.json"
-    return json.loads(prof.read_text()).get("hbm_bytes_per_launch") if prof.exists() else None
+def traffic_of(name: str, keys: int | None = None):
+    """HBM bytes per launch from the PMC pass (profiles/traffic_<name>.json), scaled to this
+    launch's key count; None without a per-key profile."""
+    d, scale = _profile("traffic", name, keys)
+    return None if d is None else d["hbm_bytes_per_launch"] * scale
 
 
-def roofline(name: str, algo_bytes: int, kern_s: float, model_insts: float) -> dict:
+def roofline(name: str, algo_bytes: int, kern_s: float, model_insts: float, keys: int | None = None) -> dict:
     achieved = algo_bytes / kern_s / 1e9
     r = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_of(name), "algorithmic_bytes_per_launch": algo_bytes}
-    r.update(valu_fields(name, kern_s, model_insts))
+         "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic_of(name, keys), "algorithmic_bytes_per_launch": algo_bytes,
+         "keys_per_launch": keys}
+    r.update(valu_fields(name, kern_s, model_insts, keys))
     return r
 
 
@@ -359,7 +413,7 @@ def secondary_csr(dev, steps, warm_ms, verify):
     algo = nbytes + 8 * n + 8 * (n + 1)
     model = sum(chunks_of(L) for L in range(lo, hi + 1)) / (hi - lo + 1) * FNV_OPS_PER_CHUNK * n / 64
     res = {"workload": CONFIGS["csr"][3], "keys": n, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
-           "value": n * steps / wall, "unit": "key hashes/s", "roofline": roofline("csr", algo, kern, model)}
+           "value": n * steps / wall, "unit": "key hashes/s", "roofline": roofline("csr", algo, kern, model, n)}
     if verify:
         res["verify"] = verify_chunks(h1, 0, _golden()["csr_8_256_64M"]["chunks"])
     del off, data, h1
@@ -383,7 +437,7 @@ def secondary_fixed(name, dev, steps, warm_ms, verify, golden_name):
     res = {"workload": desc + (" -- all 2^30 keys on one GPU" if name == "fixed32_1g" else ""), "keys": n,
            "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3, "value": n * steps / wall,
            "unit": "key hashes/s", "key_gib_per_s": n * L * steps / wall / 2**30,
-           "roofline": roofline(name, algo, kern, model)}
+           "roofline": roofline(name, algo, kern, model, n)}
     if verify:
         g = _golden()[golden_name]
         res["verify"] = verify_chunks(h1, 0, g.get("chunks") or [dict(first=0, count=g["n"], h1=g["h1"])])
@@ -410,7 +464,7 @@ def secondary_index(dev, steps, warm_ms, verify):
     model = n / 64 * chunks_of(L) * FNV_OPS_PER_CHUNK
     res = {"workload": desc + " + fused bucket index (cur_mask 2^28-1, collision_mask 0xF)", "keys": n,
            "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3, "value": n * steps / wall,
-           "unit": "key hashes + bucket positions/s", "roofline": roofline("fixed32_index", algo, kern, model)}
+           "unit": "key hashes + bucket positions/s", "roofline": roofline("fixed32_index", algo, kern, model, n)}
     if verify:
         batch.hash_fixed_index(sets[0], L, g["cur_mask"], g["collision_mask"], out=(out[0], None, out[1], out[2]))
         ok = digest_dev(out[0], 0) == g["h1"] and digest_dev(out[1], 0) == g["kindex"] and \
@@ -444,7 +498,7 @@ def secondary_ralledata(dev, steps, warm_ms, verify):
     model = sum(chunks_of(L) for L in range(klo, khi + 1)) / (khi - klo + 1) * FNV_OPS_PER_CHUNK * n / 64
     res = {"workload": desc, "records": n, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
            "value": n * steps / wall, "unit": "records/s", "blob_gb_per_s": total * steps / wall / 1e9,
-           "roofline": roofline("ralledata", algo, kern, model)}
+           "roofline": roofline("ralledata", algo, kern, model, n)}
     if verify:
         g = json.loads((ROOT / "tests" / "golden" / "ralledata_digest.json").read_text())
         ok = g["n"] == n and g["bytes"] == total and digest_dev(blob.view(torch.int64), 0) == g["blob"] and \
@@ -502,7 +556,7 @@ def secondary_import(dev, steps, warm_ms, verify):
     res = {"workload": f"{n} TSV records (keys 8-64 B, values 0-200 B, {size} B file in HBM) -> records + h1/h2",
            "records": n, "file_bytes": size, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
            "value": n * steps / wall, "unit": "records/s", "file_gb_per_s": size * steps / wall / 1e9,
-           "roofline": roofline("import", algo, wall / steps, model)}
+           "roofline": roofline("import", algo, wall / steps, model, n)}
     if verify:
         recs, h1, h2 = out["r"]
         g = json.loads((ROOT / "tests" / "golden" / "import_digest.json").read_text())
@@ -581,7 +635,12 @@ def rehearse_cpu(args, world, rank):
     import k2hash_amd
     from k2hash_amd import shard
 
-    dist.init_process_group(args.backend if args.backend != "nccl" else "gloo")
+    import datetime
+
+    dist.init_process_group(args.backend if args.backend != "nccl" else "gloo",
+                            timeout=datetime.timedelta(seconds=args.init_timeout))
+    if rank == args.inject_rank_failure:
+        os._exit(3)  # TEST ONLY (--inject-rank-failure): die before the first collective
     total = args.keys or 4096
     first, last = shard.shard_range(total, rank, world)
     raw = np.random.default_rng(1234).integers(0, 256, size=total * 32, dtype=np.uint8)[first * 32:last * 32]
@@ -640,10 +699,15 @@ def main():
     dev = torch.device("cuda", local % max(ndev, 1))  # one process per GPU; wraps only in rehearsals
     torch.cuda.set_device(dev)
     if world > 1:
+        import datetime
+
+        tmo = datetime.timedelta(seconds=args.init_timeout)
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=tmo)
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group(args.backend, timeout=tmo)
+        if rank == args.inject_rank_failure:
+            os._exit(3)  # TEST ONLY (--inject-rank-failure): die before the first collective
 
     # --- synthetic input: this rank's global key range -----------------------------------
     strong = n is None
@@ -815,7 +879,7 @@ def main():
                        "parallelism": f"shard{world}"},
             "key_gib_per_s": value * (key_bytes / n) / 2**30,
             "kernel_ms": kern_s * 1e3,
-            "roofline": roofline(prof_name, algo_bytes, kern_s, model),
+            "roofline": roofline(prof_name, algo_bytes, kern_s, model, n),
             "verify": verify,
             "cpu_baseline": cpu,
         }

@@ -89,7 +89,9 @@ int k2h_amd_hash_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uin
 
 /* Host-memory forms: same layouts, host pointers in and out.  The library stages
  * through pinned buffers and overlaps H2D / kernel / D2H in chunks on `device`.
- * Synchronous: returns when h1/h2 are filled. */
+ * Synchronous: returns when h1/h2 are filled.  The CSR form checks its offsets chunk
+ * by chunk as it streams them; offsets that decrease return K2H_AMD_EINVAL, and the
+ * contents of h1/h2 are then unspecified (earlier chunks may have been written). */
 int k2h_amd_hash_fixed_host(const void* keys, uint64_t key_len, uint64_t n, uint64_t* h1, uint64_t* h2,
                             uint32_t flags, int device);
 int k2h_amd_hash_csr_host(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1, uint64_t* h2,

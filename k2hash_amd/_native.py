@@ -12,10 +12,6 @@ from pathlib import Path
 
 LIB_DIR = Path(__file__).resolve().parent / "lib"
 BATCH_LIB = LIB_DIR / "libk2hash_amd.so"
-# Measurement lab build (tools/lab, `make -C k2hash_amd/csrc lab`): the same ABI plus the
-# round-1 A/B kernel variants behind k2h_amd_set_variant.  Selected for tools only, by
-# setting K2H_AMD_BATCH_LIB to its path before the first call; never by the product.
-LAB_LIB = Path(__file__).resolve().parents[1] / "tools" / "lab" / "libk2hash_amd_lab.so"
 PLUGIN_LIB = LIB_DIR / "libk2hfnv_plugin.so"
 
 K2H_AMD_OK = 0
@@ -93,23 +89,13 @@ def batch_lib() -> ctypes.CDLL:
             import torch  # noqa: F401
         except ImportError:
             pass
-        path = Path(os.environ.get("K2H_AMD_BATCH_LIB") or BATCH_LIB)
+        path = BATCH_LIB
         if not path.exists():
             raise RuntimeError(
                 f"k2hash_amd native library missing: {path} "
                 "(build it with `make -C k2hash_amd/csrc` or __graft_entry__.build())")
         _batch = _bind(ctypes.CDLL(str(path)), SIGNATURES.keys())
     return _batch
-
-
-def lab_set_variant(v: int) -> int:
-    """Select an A/B kernel variant -- measurement lab library only (tools/)."""
-    lib = batch_lib()
-    if not hasattr(lib, "k2h_amd_set_variant"):
-        raise RuntimeError("k2h_amd_set_variant: not the lab library (set K2H_AMD_BATCH_LIB=" + str(LAB_LIB) + ")")
-    fn = lib.k2h_amd_set_variant
-    fn.restype, fn.argtypes = ctypes.c_int, [ctypes.c_int]
-    return fn(v)
 
 
 def plugin_lib(path: str | os.PathLike | None = None) -> ctypes.CDLL:

@@ -42,6 +42,32 @@ def _check_dev(t, name: str, dtype) -> None:
         raise ValueError(f"{name} must be contiguous")
 
 
+def _check_out(t, name: str, n: int, device, torch) -> None:
+    """A caller-supplied output tensor the kernel will write n 8-byte values into: int64,
+    contiguous, on the keys' device, exactly n entries (an undersized or
+    wrong-device tensor would otherwise be written past its end by the GPU)."""
+    _check_dev(t, name, torch.int64)
+    if t.device != device:
+        raise ValueError(f"{name} is on {t.device}, the keys on {device}")
+    if t.numel() != n:
+        raise ValueError(f"{name} must have exactly {n} entries, got {t.numel()}")
+
+
+def _unpack_out(out, n: int, device, torch, second: bool, want: Tuple[str, ...]):
+    """Validate a caller's `out` tuple: h2 present iff `second`; the other named slots may be
+    None (that output is then not written)."""
+    if len(out) != len(want):
+        raise ValueError(f"out must be a tuple of {len(want)} tensors ({', '.join(want)})")
+    if out[0] is None:
+        raise ValueError("out: h1 is required")
+    if (out[1] is not None) != bool(second):
+        raise ValueError("out: pass an h2 tensor exactly when second=True")
+    for t, name in zip(out, want):
+        if t is not None:
+            _check_out(t, f"out {name}", n, device, torch)
+    return out
+
+
 def hash_fixed(keys, key_len: int, second: bool = False, std_fnv: bool = False,
                out: Optional[Tuple] = None, stream=None):
     """Hash n = keys.numel() // key_len fixed-length keys held in a uint8 device tensor.
@@ -54,7 +80,7 @@ def hash_fixed(keys, key_len: int, second: bool = False, std_fnv: bool = False,
         raise ValueError("key_len must be positive")
     n = keys.numel() // key_len
     if out is not None:
-        h1, h2 = out
+        h1, h2 = _unpack_out(out, n, keys.device, torch, second, ("h1", "h2"))
     else:
         h1 = torch.empty(n, dtype=torch.int64, device=keys.device)
         h2 = torch.empty(n, dtype=torch.int64, device=keys.device) if second else None
@@ -75,8 +101,10 @@ def hash_csr(data, offsets, second: bool = False, std_fnv: bool = False, out: Op
     n = offsets.numel() - 1
     if n < 0:
         raise ValueError("offsets must have n+1 entries")
+    if offsets.device != data.device:
+        raise ValueError("data and offsets must be on one device")
     if out is not None:
-        h1, h2 = out
+        h1, h2 = _unpack_out(out, n, data.device, torch, second, ("h1", "h2"))
     else:
         h1 = torch.empty(n, dtype=torch.int64, device=data.device)
         h2 = torch.empty(n, dtype=torch.int64, device=data.device) if second else None
@@ -108,6 +136,11 @@ def unpack_kindex(kindex):
 
 def _index_outs(torch, n, device, kindex, ckindex, out):
     if out is not None:
+        if len(out) != 2:
+            raise ValueError("out must be (kindex, ckindex)")
+        for t, name in zip(out, ("kindex", "ckindex")):
+            if t is not None:
+                _check_out(t, f"out {name}", n, device, torch)
         return out
     k = torch.empty(n, dtype=torch.int64, device=device) if kindex else None
     c = torch.empty(n, dtype=torch.int64, device=device) if ckindex else None
@@ -138,7 +171,7 @@ def hash_fixed_index(keys, key_len: int, cur_mask: int, collision_mask: int, sec
         raise ValueError("key_len must be positive")
     n = keys.numel() // key_len
     if out is not None:
-        h1, h2, k, c = out
+        h1, h2, k, c = _unpack_out(out, n, keys.device, torch, second, ("h1", "h2", "kindex", "ckindex"))
     else:
         h1 = torch.empty(n, dtype=torch.int64, device=keys.device)
         h2 = torch.empty(n, dtype=torch.int64, device=keys.device) if second else None
@@ -160,8 +193,10 @@ def hash_csr_index(data, offsets, cur_mask: int, collision_mask: int, second: bo
     n = offsets.numel() - 1
     if n < 0:
         raise ValueError("offsets must have n+1 entries")
+    if offsets.device != data.device:
+        raise ValueError("data and offsets must be on one device")
     if out is not None:
-        h1, h2, k, c = out
+        h1, h2, k, c = _unpack_out(out, n, data.device, torch, second, ("h1", "h2", "kindex", "ckindex"))
     else:
         h1 = torch.empty(n, dtype=torch.int64, device=data.device)
         h2 = torch.empty(n, dtype=torch.int64, device=data.device) if second else None

@@ -28,22 +28,6 @@ namespace {
 
 thread_local char g_err[256];
 
-#if K2H_AMD_LAB
-// Measurement lab only (tools/lab): a process-global kernel-variant knob for A/B runs.
-std::atomic<int> g_variant{-1};  // -1: read K2H_AMD_VARIANT once
-int variant() {
-  int v = g_variant.load(std::memory_order_relaxed);
-  if (v < 0) {
-    const char* e = getenv("K2H_AMD_VARIANT");
-    int want = e ? atoi(e) : 0;
-    g_variant.compare_exchange_strong(v, want);
-    v = g_variant.load(std::memory_order_relaxed);
-  }
-  return v;
-}
-#else
-constexpr int variant() { return k2h::kVariantAuto; }  // the product runs the default kernels
-#endif
 
 int fail(int code, const char* what, hipError_t e = hipSuccess) {
   if (e != hipSuccess)
@@ -289,7 +273,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed(const void* keys, 
   if (n == 0) return K2H_AMD_OK;
   if (!h1) return fail(K2H_AMD_EINVAL, "h1 is NULL");
   if (key_len && n > UINT64_MAX / key_len) return fail(K2H_AMD_EINVAL, "n * key_len overflows");
-  hipError_t e = k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream);
+  hipError_t e = k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, (hipStream_t)stream);
   if (e != hipSuccess) return fail(K2H_AMD_EHIP, "launch_fixed", e);
   return K2H_AMD_OK;
 }
@@ -299,7 +283,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr(const void* bytes, c
                                                             void* stream) {
   if (n == 0) return K2H_AMD_OK;
   if (!h1 || !offsets) return fail(K2H_AMD_EINVAL, "h1/offsets is NULL");
-  hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream);
+  hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, (hipStream_t)stream);
   if (e != hipSuccess) return fail(K2H_AMD_EHIP, "launch_csr", e);
   return K2H_AMD_OK;
 }
@@ -350,7 +334,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed_index(const void* 
   int rc = bucket_params(cur_mask, collision_mask, kindex, ckindex, bp);
   if (rc) return rc;
   hipError_t e =
-      k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream, &bp);
+      k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_fixed (index)", e);
 }
 
@@ -364,7 +348,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_index(const void* by
   k2h::BucketParams bp;
   int rc = bucket_params(cur_mask, collision_mask, kindex, ckindex, bp);
   if (rc) return rc;
-  hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, variant(), (hipStream_t)stream, &bp);
+  hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_csr (index)", e);
 }
 
@@ -399,7 +383,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed_host(const void* k
     hipError_t e = hipMemcpyAsync(s.d_in, s.h_in, cnt * key_len, hipMemcpyHostToDevice, s.stream);
     uint64_t* out = s.h_out_dev ? s.h_out_dev : s.d_out;  // kernel stores over PCIe when mapped
     if (e == hipSuccess)
-      e = k2h::launch_fixed(s.d_in, key_len, cnt, seed_for(flags), out, h2 ? out + cnt : nullptr, variant(), s.stream);
+      e = k2h::launch_fixed(s.d_in, key_len, cnt, seed_for(flags), out, h2 ? out + cnt : nullptr, s.stream);
     if (e == hipSuccess && !s.h_out_dev)
       e = hipMemcpyAsync(s.h_out, s.d_out, cnt * (h2 ? 16 : 8), hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
@@ -434,15 +418,21 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* byt
   int k = 0;
   uint64_t first = 0;
   while (first < n) {
-    // the longest run of keys from `first` within the byte budget and the key cap (>= 1 key),
-    // by binary search; the run's offsets are then checked to be non-decreasing (the GPU
-    // still works on the previous chunk meanwhile)
-    const uint64_t cap = first + kChunkKeysMax < n ? first + kChunkKeysMax : n;
-    const uint64_t limit = offsets[first] + kChunkBytes;
-    uint64_t last = (uint64_t)(std::upper_bound(offsets + first + 1, offsets + cap + 1, limit) - offsets) - 1;
-    if (last <= first) last = first + 1;
-    for (uint64_t i = first; i < last; ++i)
-      if (offsets[i + 1] < offsets[i]) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
+    // the longest run of keys from `first` within the byte budget and the key cap (>= 1
+    // key), found by a linear walk that checks every offset pair on the way: a decrease
+    // ends the call with EINVAL before any of this chunk's work is queued (the GPU still
+    // works on the previous chunk meanwhile), and no search runs over unchecked offsets
+    // (ADVICE r2).  Byte counts are differences of checked, non-decreasing offsets, so
+    // nothing wraps.
+    const uint64_t cap = n - first < kChunkKeysMax ? n : first + kChunkKeysMax;
+    if (offsets[first + 1] < offsets[first]) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
+    uint64_t last = first + 1;
+    while (last < cap) {
+      const uint64_t a = offsets[last], b = offsets[last + 1];
+      if (b < a) return fail(K2H_AMD_EINVAL, "offsets not non-decreasing");
+      if (b - offsets[first] > kChunkBytes) break;
+      ++last;
+    }
     uint64_t cnt = last - first;
     uint64_t nb = offsets[last] - offsets[first];
     Slot& s = c.slot[k];
@@ -456,7 +446,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_host(const void* byt
     if (e == hipSuccess) e = hipMemcpyAsync(s.d_off, s.h_off, (cnt + 1) * 8, hipMemcpyHostToDevice, s.stream);
     if (e == hipSuccess)
       e = k2h::launch_csr((const uint8_t*)s.d_in - offsets[first], s.d_off, cnt, seed_for(flags), s.d_out,
-                          h2 ? s.d_out + cnt : nullptr, variant(), s.stream);
+                          h2 ? s.d_out + cnt : nullptr, s.stream);
     if (e == hipSuccess) e = hipMemcpyAsync(s.h_out, s.d_out, cnt * (h2 ? 16 : 8), hipMemcpyDeviceToHost, s.stream);
     if (e == hipSuccess) e = hipEventRecord(s.done, s.stream);
     if (e != hipSuccess) return fail(K2H_AMD_EHIP, "csr host chunk", e);
@@ -478,7 +468,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_ranges(const void* base,
   if (n == 0) return K2H_AMD_OK;
   if (!h1 || !starts || !lens || !base) return fail(K2H_AMD_EINVAL, "NULL base/starts/lens/h1");
   hipError_t e = k2h::launch_ranges(base, starts, lens, n, seed_for(flags), (flags & K2H_AMD_FLAG_CSTR) != 0, h1, h2,
-                                    variant(), (hipStream_t)stream);
+                                    (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_ranges", e);
 }
 
@@ -542,7 +532,7 @@ __attribute__((visibility("default"))) int k2h_amd_build_ralledata(
   in.soff = skey_off;
   in.attrs = (const uint8_t*)attrs;
   in.aoff = attr_off;
-  hipError_t e = k2h::launch_ralledata(in, n, seed_for(flags), (uint8_t*)out, blob_off, variant(), (hipStream_t)stream);
+  hipError_t e = k2h::launch_ralledata(in, n, seed_for(flags), (uint8_t*)out, blob_off, (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_ralledata", e);
 }
 
@@ -593,7 +583,7 @@ __attribute__((visibility("default"))) int k2h_amd_build_ralledata_host(
   }
   if (e == hipSuccess) e = hipMallocAsync((void**)&dout, total, st);
   if (e == hipSuccess && blob_off) e = hipMallocAsync((void**)&dblob, (n + 1) * 8, st);
-  if (e == hipSuccess) e = k2h::launch_ralledata(in, n, seed_for(flags), dout, dblob, variant(), st);
+  if (e == hipSuccess) e = k2h::launch_ralledata(in, n, seed_for(flags), dout, dblob, st);
   if (e == hipSuccess) e = hipMemcpyAsync(out, dout, total, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess && blob_off) e = hipMemcpyAsync(blob_off, dblob, (n + 1) * 8, hipMemcpyDeviceToHost, st);
   for (int s = 0; s < 4; ++s) {
@@ -620,10 +610,6 @@ __attribute__((visibility("default"))) const char* k2h_amd_strerror(int code) {
   return "unknown error";
 }
 
-#if K2H_AMD_LAB
-__attribute__((visibility("default"))) int k2h_amd_set_variant(int v) { return g_variant.exchange(v); }
-__attribute__((visibility("default"))) int k2h_amd_get_variant(void) { return variant(); }
-#endif
 
 __attribute__((visibility("default"))) int k2h_amd_synth_bytes(void* out, uint64_t nbytes, uint64_t seed,
                                                                uint64_t byte_off, void* stream) {

@@ -36,44 +36,6 @@ typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
 __device__ __forceinline__ uint64_t seg_len(const uint64_t* off, uint64_t i) { return off ? off[i + 1] - off[i] : 0; }
 __device__ __forceinline__ uint64_t seg_before(const uint64_t* off, uint64_t i) { return off ? off[i] - off[0] : 0; }
 
-#if K2H_AMD_LAB  // one thread per record (A/B variant)
-__device__ __forceinline__ void copy_bytes(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len) {
-  uint64_t j = 0;
-  for (; j + 16 <= len; j += 16) *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
-  for (; j < len; ++j) dst[j] = src[j];
-}
-
-
-__global__ __launch_bounds__(256) void ralledata_assemble_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
-                                                                 uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
-  uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i), al = seg_len(in.aoff, i);
-  const uint64_t o = 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) +
-                     seg_before(in.aoff, i);
-  uint8_t* b = out + o;
-  u64_ua* hd = reinterpret_cast<u64_ua*>(b);
-  hd[0] = h[i];
-  hd[1] = h[n + i];
-  hd[2] = kl;
-  hd[3] = vl;
-  hd[4] = sl;
-  hd[5] = al;
-  hd[6] = 80;
-  hd[7] = 80 + kl;
-  hd[8] = 80 + kl + vl;
-  hd[9] = 80 + kl + vl + sl;
-  if (kl) copy_bytes(b + 80, in.keys + in.koff[i], kl);
-  if (vl) copy_bytes(b + 80 + kl, in.vals + in.voff[i], vl);
-  if (sl) copy_bytes(b + 80 + kl + vl, in.skeys + in.soff[i], sl);
-  if (al) copy_bytes(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al);
-  if (blob_off) {
-    blob_off[i] = o;
-    if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
-  }
-}
-
-#endif
 
 // Group form (default): G lanes per record, 64/G records per wave.  Lane q of a group
 // writes header piece q (5 x 16 B) and copies bytes [16q + 16Gj, +16) of each segment,
@@ -445,8 +407,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
       for (int k = max(0, -x); k < 16 && x + k < sp; ++k) base[16ull * p + k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
     }
   };
+  // A piece's next segment is read before it is known to reach into the piece (the read is
+  // then discarded), and its window can fall outside the image (e.g. a long pool segment
+  // followed by the next record's header): clamp the index into the image.
   auto window = [&](int2 sg, uint32_t p) {
-    return *reinterpret_cast<const u32x4_ua*>(img + sg.x + 16 * (int32_t)p - d0);
+    const int32_t at = min(max(sg.x + 16 * (int32_t)p - d0, 0), kGatherImg - 16);
+    return *reinterpret_cast<const u32x4_ua*>(img + at);
   };
   if constexpr (PU == 2) {  // two pieces per trip: their LDS reads in flight together
     for (uint32_t p = tid; p < np; p += 512) {
@@ -477,298 +443,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
   }
 }
 
-#if K2H_AMD_LAB
-// Staged form (round-2 A/B variant 65, measured SLOWER: 2.14 vs 1.50 ms on 8M records --
-// the LDS round trip and the block barrier cost more than the unaligned HBM stores): a block assembles the blobs of RPB consecutive records in
-// an LDS image of their packed output span -- headers and segment pieces written at their
-// (unaligned) blob positions, as the group form writes them to HBM -- then stores the span
-// as aligned 16-byte pieces, consecutive lanes on consecutive pieces, i.e. whole 128-byte
-// lines; only the two pieces a block shares with its neighbours are written byte by byte.
-// The group form's unaligned 16-byte stores straight to HBM ran at ~2.3 TB/s.  A block
-// whose span exceeds the image (records far larger than BASELINE-like ones) assembles
-// straight to HBM like the group form.
-template <int G>
-__device__ __forceinline__ void group_copy_lds(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
-                                               uint64_t len, uint32_t q) {
-  const uint64_t full = len & ~15ull;
-  for (uint64_t j = 16ull * q; j < full; j += 16ull * G)
-    *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
-  if (full == len) return;
-  if (len >= 16) {
-    if (q == G - 1) *reinterpret_cast<u32x4_ua*>(dst + len - 16) = *reinterpret_cast<const u32x4_ua*>(src + len - 16);
-    return;
-  }
-  for (uint64_t t = q; t < len; t += G) dst[t] = src[t];
-}
-
-__device__ __forceinline__ uint64_t blob_start(const RalleInputs& in, uint64_t i) {
-  return 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) + seg_before(in.aoff, i);
-}
-
-template <int RPB, int IMG>
-__global__ __launch_bounds__(256) void ralledata_stage_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
-                                                              uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
-  constexpr int G = 8, NG = 256 / G;
-  __shared__ __attribute__((aligned(16))) uint8_t img[IMG];
-  const uint32_t tid = threadIdx.x, q = tid % G, grp = tid / G;
-  const uint64_t r0 = (uint64_t)blockIdx.x * RPB;
-  const uint32_t nr = (uint32_t)(n - r0 < (uint64_t)RPB ? n - r0 : (uint64_t)RPB);
-  const uint64_t o_first = blob_start(in, r0), o_end = blob_start(in, r0 + nr);
-  const uint64_t a0 = o_first & ~15ull;
-  const bool staged = o_end - a0 <= (uint64_t)IMG;  // block-uniform
-  // one record's blob at b (LDS image or HBM: two inlined copies, so each writes through its
-  // own address space instead of flat stores)
-  auto assemble = [&](uint8_t* __restrict__ b, uint64_t i, uint64_t kl, uint64_t vl, uint64_t sl, uint64_t al) {
-    if (q < 5) {
-      uint64_t f0, f1;
-      switch (q) {
-        case 0: f0 = h[i]; f1 = h[n + i]; break;
-        case 1: f0 = kl; f1 = vl; break;
-        case 2: f0 = sl; f1 = al; break;
-        case 3: f0 = 80; f1 = 80 + kl; break;
-        default: f0 = 80 + kl + vl; f1 = 80 + kl + vl + sl; break;
-      }
-      *reinterpret_cast<u32x4_ua*>(b + 16 * q) =
-          u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
-    }
-    if (kl) group_copy_lds<G>(b + 80, in.keys + in.koff[i], kl, q);
-    if (vl) group_copy_lds<G>(b + 80 + kl, in.vals + in.voff[i], vl, q);
-    if (sl) group_copy_lds<G>(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
-    if (al) group_copy_lds<G>(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
-  };
-  for (uint32_t rec = grp; rec < nr; rec += NG) {
-    const uint64_t i = r0 + rec;
-    const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i),
-                   al = seg_len(in.aoff, i);
-    const uint64_t o = blob_start(in, i);
-    if (staged) assemble(img + (uint32_t)(o - a0), i, kl, vl, sl, al);
-    else assemble(out + o, i, kl, vl, sl, al);
-    if (blob_off && q == 0) {
-      blob_off[i] = o;
-      if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
-    }
-  }
-  if (!staged) return;
-  __syncthreads();
-  // pieces [a0 + 16 p, +16); the first and the last may hold a neighbour's bytes
-  const uint32_t np = (uint32_t)((o_end - a0 + 15) >> 4);
-  typedef uint32_t u32x4_al __attribute__((ext_vector_type(4)));
-  for (uint32_t p = tid; p < np; p += 256) {
-    const uint64_t lo = a0 + 16ull * p;
-    if (lo >= o_first && lo + 16 <= o_end) {
-      __builtin_nontemporal_store(*reinterpret_cast<const u32x4_al*>(img + 16 * p),
-                                  reinterpret_cast<u32x4_al*>(out + lo));
-    } else {
-      for (uint32_t j = 0; j < 16; ++j)
-        if (lo + j >= o_first && lo + j < o_end) out[lo + j] = img[16 * p + j];
-    }
-  }
-}
-
-#endif  // K2H_AMD_LAB
-
-#if K2H_AMD_LAB
-// Batched form (A/B variants 57-58, measured slower: 1.56 ms at 2 and 2.13 ms at 4 records
-// per group vs 1.50 for the group form -- the register cost (82 / 152 VGPRs) outweighs the
-// extra loads in flight).  Motivation: a header-only probe of the group form already
-// takes 0.62 of its 1.43 ms, so its waves look latency bound.  Here a
-// group of G lanes takes RPG consecutive records: all their offsets are loaded
-// together, and each segment is copied for all RPG records with straight-line,
-// predicated code (pieces 16q and 16q + 16G, the overlapped tail, short segments byte by
-// byte), so the loads of every record are in flight before the first store.  Pieces
-// beyond 32G bytes of a segment take a loop.
-template <int G, int RPG>
-__global__ __launch_bounds__(256) void ralledata_batch_kernel(RalleInputs in, uint64_t n,
-                                                              const uint64_t* __restrict__ h,
-                                                              uint8_t* __restrict__ out,
-                                                              uint64_t* __restrict__ blob_off) {
-  static_assert(G >= 8 && 64 % G == 0, "five lanes write the header, eight cover a short segment");
-  const uint64_t grp = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / G;
-  const uint32_t q = threadIdx.x % G;
-  if (grp * RPG >= n) return;
-  const uint64_t* offs[4] = {in.koff, in.voff, in.soff, in.aoff};
-  const uint8_t* bases[4] = {in.keys, in.vals, in.skeys, in.attrs};
-  uint64_t o0[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) o0[s] = offs[s] ? offs[s][0] : 0;
-
-  bool ok[RPG];
-  uint64_t rec[RPG], o[RPG];
-  uint32_t len[RPG][4];
-  uint64_t src[RPG][4];
-#pragma unroll
-  for (int r = 0; r < RPG; ++r) {
-    rec[r] = grp * RPG + r;
-    ok[r] = rec[r] < n;
-    const uint64_t i = ok[r] ? rec[r] : n - 1;
-    uint64_t ob = 80ull * i;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      uint64_t b = offs[s] ? offs[s][i] : 0, e = offs[s] ? offs[s][i + 1] : 0;
-      len[r][s] = (uint32_t)(e - b);
-      src[r][s] = (uint64_t)(uintptr_t)bases[s] + b;
-      ob += b - o0[s];
-    }
-    o[r] = ob;
-  }
-  // headers + blob offsets
-#pragma unroll
-  for (int r = 0; r < RPG; ++r) {
-    if (!ok[r]) continue;
-    uint8_t* b = out + o[r];
-    const uint64_t kl = len[r][0], vl = len[r][1], sl = len[r][2], al = len[r][3];
-    if (q < 5) {
-      uint64_t f0, f1;
-      switch (q) {
-        case 0: f0 = h[rec[r]]; f1 = h[n + rec[r]]; break;
-        case 1: f0 = kl; f1 = vl; break;
-        case 2: f0 = sl; f1 = al; break;
-        case 3: f0 = 80; f1 = 80 + kl; break;
-        default: f0 = 80 + kl + vl; f1 = 80 + kl + vl + sl; break;
-      }
-      *reinterpret_cast<u32x4_ua*>(b + 16 * q) =
-          u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
-    }
-    if (blob_off && q == 0) {
-      blob_off[rec[r]] = o[r];
-      if (rec[r] + 1 == n) blob_off[n] = o[r] + 80 + kl + vl + sl + al;
-    }
-  }
-  // segments, one after the other (a compiler barrier between them keeps the loads of
-  // one segment for all RPG records together without hoisting every segment's loads)
-  auto segment = [&](const int s) {
-    u32x4_ua pa[RPG], pb[RPG], pt[RPG];
-    uint8_t c0[RPG], c1[RPG];
-#pragma unroll
-    for (int r = 0; r < RPG; ++r) {  // loads
-      const uint32_t L = ok[r] ? len[r][s] : 0u, full = L & ~15u;
-      const uint8_t* sp = (const uint8_t*)(uintptr_t)src[r][s];
-      if (16u * q < full) pa[r] = *reinterpret_cast<const u32x4_ua*>(sp + 16u * q);
-      if (16u * (q + G) < full) pb[r] = *reinterpret_cast<const u32x4_ua*>(sp + 16u * (q + G));
-      if (L >= 16u && (L & 15u) && q == G - 1) pt[r] = *reinterpret_cast<const u32x4_ua*>(sp + L - 16u);
-      if (L < 16u) {
-        if (q < L) c0[r] = sp[q];
-        if (q + G < L) c1[r] = sp[q + G];
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < RPG; ++r) {  // stores
-      const uint32_t L = ok[r] ? len[r][s] : 0u, full = L & ~15u;
-      uint32_t before = 80u;
-      for (int t = 0; t < s; ++t) before += len[r][t];
-      uint8_t* dp = out + o[r] + before;
-      if (16u * q < full) *reinterpret_cast<u32x4_ua*>(dp + 16u * q) = pa[r];
-      if (16u * (q + G) < full) *reinterpret_cast<u32x4_ua*>(dp + 16u * (q + G)) = pb[r];
-      if (L >= 16u && (L & 15u) && q == G - 1) *reinterpret_cast<u32x4_ua*>(dp + L - 16u) = pt[r];
-      if (L < 16u) {
-        if (q < L) dp[q] = c0[r];
-        if (q + G < L) dp[q + G] = c1[r];
-      }
-      const uint8_t* sp = (const uint8_t*)(uintptr_t)src[r][s];
-      for (uint32_t j = 16u * (q + 2 * G); j < full; j += 16u * G)  // long segments
-        *reinterpret_cast<u32x4_ua*>(dp + j) = *reinterpret_cast<const u32x4_ua*>(sp + j);
-    }
-    asm volatile("" ::: "memory");
-  };
-  if (in.koff) segment(0);
-  if (in.voff) segment(1);
-  if (in.soff) segment(2);
-  if (in.aoff) segment(3);
-}
-
-#endif  // K2H_AMD_LAB
-
 }  // namespace
 
-#if K2H_AMD_LAB
-constexpr int kRalleRecsPerBlock = 64;   // ~16 KB of blobs for BASELINE-like records (80 + 8-64 + 0-256 B)
-constexpr int kRalleImage = 32 * 1024;   // 4 blocks per CU; spans above it assemble straight to HBM
-#endif
-
 hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, uint8_t* out, uint64_t* blob_off,
-                            int variant, hipStream_t stream) {
+                            hipStream_t stream) {
   if (n == 0) {
     if (blob_off) return hipMemsetAsync(blob_off, 0, 8, stream);
     return hipSuccess;
   }
-#if K2H_AMD_LAB
-  const bool two_kernels = variant == kVariantRalleThread || variant == kVariantRalleProbeAligned ||
-                           variant == kVariantRalleProbeHeader || variant == kVariantRalleGroup16 ||
-                           variant == kVariantRalleByteTail || variant == kVariantRalleBatch4 ||
-                           variant == kVariantRalleBatch2 || variant == kVariantRalleStage ||
-                           variant == kVariantRalleGroup8 || variant == kVariantRalleGather;
-#else
-  constexpr bool two_kernels = false;
-#endif
-#if K2H_AMD_LAB
-  if (variant == kVariantRalleStageAll) {
-    ralledata_gather_kernel<true, 0, 1, true>
-        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
-    return hipGetLastError();
-  }
-  if (variant == kVariantRallePrioLoads || variant == kVariantRallePrioPhase1) {
-    if (variant == kVariantRallePrioLoads)
-      ralledata_gather_kernel<true, 0, 1, false, 1>
-          <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
-    else
-      ralledata_gather_kernel<true, 0, 1, false, 2>
-          <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
-    return hipGetLastError();
-  }
-  if (variant == kVariantRallePieces2) {
-    ralledata_gather_kernel<true, 0, 2>
-        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
-    return hipGetLastError();
-  }
-  if (variant == kVariantRallePhasesNoStore) {
-    ralledata_gather_kernel<true, 2>
-        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
-    return hipGetLastError();
-  }
-  if (variant == kVariantRallePhases) {
-    ralledata_gather_kernel<true, 1>
-        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
-    return hipGetLastError();
-  }
-#endif
-  if (!two_kernels) {  // the product: one kernel, hashes computed from the staged keys
-    ralledata_gather_kernel<true>
-        <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
-    return hipGetLastError();
-  }
-#if K2H_AMD_LAB
-  // lab: the CSR hash kernel writes h1/h2 to stream-ordered scratch, then an assembly kernel
-  uint64_t* h = nullptr;
-  hipError_t e = hipMallocAsync((void**)&h, 16 * n, stream);
-  if (e != hipSuccess) return e;
-  e = launch_csr(in.keys, in.koff, n, seed, h, h + n, variant, stream);
-  if (e == hipSuccess) {
-    if (variant == kVariantRalleThread)
-      ralledata_assemble_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else if (variant == kVariantRalleProbeAligned)
-      ralledata_group_kernel<8, false, 1><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else if (variant == kVariantRalleProbeHeader)
-      ralledata_group_kernel<8, false, 2><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else if (variant == kVariantRalleGroup16)
-      ralledata_group_kernel<16><<<(unsigned)((n * 16 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else if (variant == kVariantRalleByteTail)
-      ralledata_group_kernel<16, true><<<(unsigned)((n * 16 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else if (variant == kVariantRalleBatch4)
-      ralledata_batch_kernel<8, 4><<<(unsigned)(((n + 3) / 4 * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else if (variant == kVariantRalleBatch2)
-      ralledata_batch_kernel<8, 2><<<(unsigned)(((n + 1) / 2 * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else if (variant == kVariantRalleStage)
-      ralledata_stage_kernel<kRalleRecsPerBlock, kRalleImage>
-          <<<(unsigned)((n + kRalleRecsPerBlock - 1) / kRalleRecsPerBlock), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else if (variant == kVariantRalleGroup8)
-      ralledata_group_kernel<8><<<(unsigned)((n * 8 + 255) / 256), 256, 0, stream>>>(in, n, h, out, blob_off);
-    else
-      ralledata_gather_kernel<false><<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, h, out, blob_off, SpadTable{});
-    e = hipGetLastError();
-  }
-  hipError_t f = hipFreeAsync(h, stream);
-  return e != hipSuccess ? e : f;
-#endif
+  // one kernel, the key hashes computed from the staged keys
+  ralledata_gather_kernel<true>
+      <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+  return hipGetLastError();
 }
 
 }  // namespace k2h

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(256) void cstr_fixup_kernel(const uint64_t* __restr
 }  // namespace
 
 hipError_t launch_ranges(const void* base, const uint64_t* starts, const uint64_t* lens, uint64_t n, uint64_t seed,
-                         bool cstr, uint64_t* h1, uint64_t* h2, int variant, hipStream_t stream) {
+                         bool cstr, uint64_t* h1, uint64_t* h2, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   // offsets[0] = 0, offsets[i+1] = sum of lens[0..i]
   uint64_t* off = nullptr;
@@ -81,7 +81,7 @@ hipError_t launch_ranges(const void* base, const uint64_t* starts, const uint64_
     e = hipGetLastError();
   }
   // the CSR kernels treat a NULL byte buffer as "all keys empty"; packed is never NULL here
-  if (e == hipSuccess) e = launch_csr(packed, off, n, seed, h1, cstr ? nullptr : h2, variant, stream);
+  if (e == hipSuccess) e = launch_csr(packed, off, n, seed, h1, cstr ? nullptr : h2, stream);
   if (e == hipSuccess && cstr) {
     cstr_fixup_kernel<<<(unsigned)((n + 255) / 256), 256, 0, stream>>>(lens, n, seed, h1, h2);
     e = hipGetLastError();

@@ -39,6 +39,47 @@ def test_launcher_rehearsal_cpu_three_ranks():
     assert line["n_gpus"] == 3 and line["gather"]["ok"] is True
 
 
+def test_launcher_fails_fast_when_a_rank_dies():
+    """A rank that dies after joining the process group (--inject-rank-failure, test only)
+    must end the whole run with a non-zero status well inside the driver's limit, with no
+    rank left running (rank 0 would otherwise block in its first collective)."""
+    import time
+
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    t0 = time.monotonic()
+    p = subprocess.run([sys.executable, str(ROOT / "bench.py"), "--gpus", "3", "--rehearse-cpu", "--backend", "gloo",
+                        "--steps", "1", "--warmup", "0", "--keys", "99", "--inject-rank-failure", "1",
+                        "--init-timeout", "300"], capture_output=True, text=True, timeout=120, env=env)
+    took = time.monotonic() - t0
+    assert p.returncode != 0 and took < 60, (p.returncode, took, p.stderr[-2000:])
+    assert "rank 1 exited with 3" in p.stderr
+    pids = [int(x) for x in p.stderr.split("rank pids [", 1)[1].split("]", 1)[0].split(",")]
+    time.sleep(0.5)
+    for pid in pids:
+        try:
+            os.kill(pid, 0)
+            alive = Path(f"/proc/{pid}/status").read_text().split("State:")[1].split()[0] != "Z"
+        except (ProcessLookupError, FileNotFoundError, IndexError):
+            alive = False
+        assert not alive, f"rank process {pid} survived the launcher"
+
+
+def test_roofline_fields_scale_with_keys_per_launch():
+    """roofline.traffic / valu_frac come from profiles taken at one key count; a launch of
+    another size (config 4 at N = 8: 2^27 keys per rank) must be scaled, not copied."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    n = 1 << 27
+    algo = 40 * n
+    r = bench.roofline("fixed32_1g", algo, 0.94e-3, 0.0, n)
+    assert r["traffic"] is not None and 0.99 < r["traffic"] / algo < 1.05
+    assert 0.3 < r["valu_frac"] < 1.0
+    full = bench.roofline("fixed32_1g", 40 << 30, 7.4e-3, 0.0, 1 << 30)
+    assert abs(full["valu_insts_per_launch"] / r["valu_insts_per_launch"] - 8.0) < 1e-9
+    assert bench.roofline("fixed32_1g", algo, 1e-3, 123.0, None)["traffic"] is None
+
+
 @pytest.mark.gpu
 def test_bench_two_ranks_one_gpu():
     """Config 4's path at N=2 on one card: strong-scaled shards of a small key count, the
@@ -47,6 +88,11 @@ def test_bench_two_ranks_one_gpu():
                  "--warm-ms", "5"], 600)
     assert line["n_gpus"] == 2 and line["scaling"] == "strong"
     assert line["gather"]["with_gather"]["value"] > 0 and line["gather"]["backend"] == "gloo"
+    # profile-derived fields are scaled to this launch's key count
+    rf = line["roofline"]
+    assert rf["keys_per_launch"] == 262144
+    assert 0 < rf["valu_frac"] < 1.2
+    assert rf["traffic"] is None or rf["traffic"] / rf["algorithmic_bytes_per_launch"] < 1.2
 
 
 @pytest.mark.gpu

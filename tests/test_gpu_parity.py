@@ -271,3 +271,39 @@ def test_host_api_error_mid_call_leaves_no_stale_chunk(cuda, oracle):
     assert np.array_equal(h1, r1) and np.array_equal(h2, r2)
     g1, _ = k2hash_amd.hash_csr_host(data, off)  # and the full call still works
     assert np.array_equal(g1, oracle.hash_csr(data, off)[0])
+
+
+def test_out_tensors_validated(cuda, oracle):
+    """Caller-supplied output tensors are checked before the kernel writes n values into
+    them: undersized, wrong dtype, non-contiguous, h2 given without second=True
+    (or missing with it) -> ValueError, nothing launched."""
+    import torch
+    n = 1000
+    data = oracle.gen_bytes(32 * n)
+    keys = dev_u8(torch, data, cuda)
+    ok = torch.empty(n, dtype=torch.int64, device=cuda)
+    bad = [
+        (torch.empty(n - 1, dtype=torch.int64, device=cuda), None),
+        (torch.empty(n, dtype=torch.int32, device=cuda), None),
+        (torch.empty(2 * n, dtype=torch.int64, device=cuda)[::2], None),
+        (torch.empty(n, dtype=torch.int64), None),
+    ]
+    for out in bad:
+        with pytest.raises(ValueError):
+            k2hash_amd.hash_fixed(keys, 32, out=out)
+    with pytest.raises(ValueError):
+        k2hash_amd.hash_fixed(keys, 32, out=(ok, torch.empty(n, dtype=torch.int64, device=cuda)))
+    with pytest.raises(ValueError):
+        k2hash_amd.hash_fixed(keys, 32, second=True, out=(ok, None))
+    off = torch.arange(0, 32 * n + 1, 32, dtype=torch.int64, device=cuda)
+    with pytest.raises(ValueError):
+        k2hash_amd.hash_csr(keys, off, out=(torch.empty(n - 1, dtype=torch.int64, device=cuda), None))
+    with pytest.raises(ValueError):
+        batch.hash_fixed_index(keys, 32, 0xFF, 0xF, out=(ok, None, torch.empty(7, dtype=torch.int64, device=cuda), None))
+    with pytest.raises(ValueError):
+        batch.hash_csr_index(keys, off, 0xFF, 0xF, out=(ok, None, None, torch.empty(n + 1, dtype=torch.int64, device=cuda)))
+    with pytest.raises(ValueError):
+        batch.bucket_index(ok, 0xFF, 0xF, out=(torch.empty(n - 1, dtype=torch.int64, device=cuda), None))
+    h1, _ = k2hash_amd.hash_fixed(keys, 32, out=(ok, None))  # the valid form still works
+    torch.cuda.synchronize()
+    assert np.array_equal(host_u64(h1), oracle.hash_fixed(data, 32)[0])

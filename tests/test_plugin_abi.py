@@ -56,8 +56,10 @@ def test_product_library_has_no_lab_code():
         assert name.encode() not in blob, name
     lib = ctypes.CDLL(str(_native.BATCH_LIB))
     assert not hasattr(lib, "k2h_amd_set_variant") and not hasattr(lib, "k2h_amd_get_variant")
-    # the product CSR path is the lean2 tile kernel plus the ring pass for oversize tiles
-    assert b"fnv_csr_lean2_kernel" in blob and b"fnv_csr_ring_list_kernel" in blob
+    # the product CSR path is one kernel: staged tiles, oversize tiles on the line ring in
+    # the same block (no second launch, no scratch list)
+    assert b"fnv_csr_staged_kernel" in blob
+    assert b"fnv_csr_ring_list_kernel" not in blob and b"fnv_csr_lean2_kernel" not in blob
 
 
 def test_plugin_has_no_hip_dependency():
