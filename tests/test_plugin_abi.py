@@ -194,3 +194,51 @@ def test_python_mirror_scalar():
     assert k2hash_amd.k2h_second_hash(b"KEY-0000000000000000\0") == 0x1bfb06d77c7f9f13
     assert k2hash_amd.k2h_hash(None) == 0 and k2hash_amd.k2h_hash(b"") == 0
     assert k2hash_amd.k2h_hash_version() == "FNV-1A BUILTIN"
+
+
+# ---------------------------------------------------------------------------
+# The interposition route: libk2hash carries the weak builtins in the same
+# shared library as their call sites (lib/k2hcommon.h:41-45, lib/k2hashfunc.h:65-72), and
+# k2hbench can only pick up a plugin by link-time override or LD_PRELOAD.  oracle/_ref/
+# libk2hcaller_ref.so = the reference's lib/k2hashfunc.cc + lib/k2hdbg.cc + call sites
+# written like K2HShm's (K2H_HASH_FUNC / K2H_2ND_HASH_FUNC, k2h_hash_version() for the
+# file stamp); the driver reports which object its k2h_hash resolved to (dladdr).
+# ---------------------------------------------------------------------------
+def _interpose(preload, vectors):
+    from oracle import REF
+    drv = REF / "interpose_driver"
+    if not drv.exists():
+        pytest.skip("reference build unavailable")
+    env = dict(os.environ)
+    if preload:  # prepend: keep whatever the environment already preloads
+        env["LD_PRELOAD"] = ":".join([str(preload)] + ([env["LD_PRELOAD"]] if env.get("LD_PRELOAD") else []))
+    keys = [v for v in vectors["vectors"]][:64]
+    stdin = "".join((v["key"] or "-") + "\n" for v in keys)
+    out = subprocess.run([str(drv)], input=stdin, capture_output=True, text=True, env=env, check=True).stdout
+    lines = out.splitlines()
+    fn = lines[0].split(" ", 1)[1]
+    ver = lines[1].split(" ", 1)[1]
+    got = [tuple(int(x, 16) for x in ln.split()) for ln in lines[2:]]
+    want = [(u64(v["h1"]), u64(v["h2"])) for v in keys]
+    return fn, ver, got, want
+
+
+def test_interposition_reaches_the_plugin(vectors):
+    fn, ver, got, want = _interpose(None, vectors)
+    assert fn.endswith("libk2hcaller_ref.so") and ver == "FNV-1A BUILTIN" and got == want
+    for so in (_native.PLUGIN_LIB, _native.BATCH_LIB):
+        fn, ver, got, want = _interpose(so, vectors)
+        assert Path(fn).resolve() == Path(so).resolve(), fn  # the call sites bind to the plugin
+        assert ver == "FNV-1A BUILTIN"  # the stamp keeps existing files attachable
+        assert got == want
+
+
+def test_interposition_control_sample_plugin(vectors):
+    """Control: preloading the reference's own sample plugin (tests/k2htesthashfunc.cc,
+    "DSO HASH V1.0") changes the call sites' results -- the route is live, so the equal
+    hashes above come from our plugin, not from the builtins."""
+    from oracle import REF_TESTHASH_SO
+    if not REF_TESTHASH_SO.exists():
+        pytest.skip("reference build unavailable")
+    fn, ver, got, want = _interpose(REF_TESTHASH_SO, vectors)
+    assert fn.endswith("libk2htesthash_ref.so") and ver == "DSO HASH V1.0" and got != want
