@@ -55,19 +55,23 @@ for d in sorted(p for p in src.iterdir() if p.is_dir() and "_pmc" not in p.name)
                 pmc.setdefault(c, []).append(v)
     pmc = {k: sum(v) / len(v) for k, v in pmc.items()}
     traffic = None
+    # keys (records) per launch of the profiled kernel: bench.py scales the per-launch counts
+    # to other launch sizes by it
+    keys = (line or {}).get("config", {}).get("keys_per_gpu")
     if "FETCH_SIZE" in pmc and "WRITE_SIZE" in pmc:
         traffic = int(2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024)
         (dst / f"traffic_{cfg}.json").write_text(json.dumps({
             "kernel": top["Name"], "hbm_bytes_per_launch": traffic, "FETCH_SIZE_kB": pmc["FETCH_SIZE"],
             "WRITE_SIZE_kB": pmc["WRITE_SIZE"], "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
-            "source": f"profiles/{tag}_{cfg}_summary.json (rocprofv3 --pmc passes)", "round": tag}, indent=1))
+            "source": f"profiles/{tag}_{cfg}_summary.json (rocprofv3 --pmc passes)", "round": tag,
+            "keys_per_launch": keys}, indent=1))
     if "SQ_INSTS_VALU" in pmc:
         (dst / f"valu_{cfg}.json").write_text(json.dumps({
             "kernel": top["Name"], "valu_insts_per_launch": pmc["SQ_INSTS_VALU"],
             "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"), "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"),
             "waves_per_launch": pmc.get("SQ_WAVES"),
-            "source": f"profiles/{tag}_{cfg}_summary.json (rocprofv3 --pmc SQ_INSTS_VALU pass)", "round": tag},
-            indent=1))
+            "source": f"profiles/{tag}_{cfg}_summary.json (rocprofv3 --pmc SQ_INSTS_VALU pass)", "round": tag,
+            "keys_per_launch": keys}, indent=1))
     s = {"window": window, "pmc_per_launch": pmc, "hbm_bytes_per_launch": traffic}
     if line:
         kern_ms = line["kernel_ms"]
