@@ -263,6 +263,55 @@ def cpu_baseline(keys_host, key_len: int, n: int) -> dict | None:
     }
 
 
+def cpu_baseline_workload(kind: str, host_bytes, host_off, key_len: int, n1: int, n: int, gpu_h1=None) -> dict:
+    """The reference's k2h_hash (oracle/_ref via dlsym, else the C restatement) over a
+    bounded prefix of a secondary config's exact input (SURVEY 8d CPU row ii):
+    the first n1 keys on 1 thread and the first n keys on the usable cores (one shard of
+    about equal bytes per parked worker thread), h1 only, best of 3 runs of `passes`
+    passes.  key GB/s = key bytes hashed / s.  gpu_h1: the GPU's h1 of the same keys, checked
+    against the CPU pass's xor-digest."""
+    import ctypes
+
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle  # test/baseline infrastructure only
+
+    lib = oracle.cpubench()
+    so = str(oracle.REF_SO) if oracle.REF_SO.exists() else ""
+    info = host_info()
+    cores = usable_cores(info)
+    dig = ctypes.c_uint64()
+    bptr = ctypes.c_void_p(host_bytes.ctypes.data)
+
+    def run(m, threads, passes):
+        if kind == "csr":
+            optr = ctypes.c_void_p(host_off.ctypes.data)
+            ts = [lib.cpu_bench_csr(so.encode(), bptr, optr, m, threads, passes, 0, ctypes.byref(dig)) for _ in range(3)]
+            nbytes = int(host_off[m] - host_off[0])
+        else:
+            ts = [lib.cpu_bench_fixed(so.encode(), bptr, key_len, m, threads, passes, 0, ctypes.byref(dig))
+                  for _ in range(3)]
+            nbytes = m * key_len
+        t = min(ts) / passes
+        return {"threads": threads, "keys": m, "key_bytes": nbytes, "seconds_per_pass": t, "value": m / t,
+                "key_gb_per_s": nbytes / t / 1e9}
+
+    one = run(n1, 1, 2)
+    many = run(n, cores, 2)
+    res = {"kind": "reference" if so else "port", "unit": "key hashes/s", "single_thread": one, "cores": many,
+           "value": many["value"], "cores_used": cores,
+           "sample": f"first {n1} keys on 1 thread, first {n} keys on {cores} threads (the box's CPU share), "
+                     "h1 only, 2 passes per run, best of 3 runs; reference lib/k2hashfunc.cc k2h_hash via dlsym"}
+    if gpu_h1 is not None and kind == "csr":  # the CPU digest (one pass, n keys) against the GPU's hashes
+        lib.cpu_bench_csr(so.encode(), bptr, ctypes.c_void_p(host_off.ctypes.data), n, 1, 1, 0, ctypes.byref(dig))
+        res["digest_matches_gpu"] = int(np.bitwise_xor.reduce(gpu_h1.view(np.uint64))) == dig.value
+    elif gpu_h1 is not None:
+        lib.cpu_bench_fixed(so.encode(), bptr, key_len, n, 1, 1, 0, ctypes.byref(dig))
+        res["digest_matches_gpu"] = int(np.bitwise_xor.reduce(gpu_h1.view(np.uint64))) == dig.value
+    return res
+
+
 # --------------------------------------------------------------------------------------
 # Digests of the reference's outputs (tests/golden/digests.json): [xor, wrapping sum,
 # wrapping sum of h*(2i+1)], i = global key index.  Computed on the device.
@@ -398,7 +447,8 @@ def chunks_of(length: int) -> int:
 # --------------------------------------------------------------------------------------
 # Secondary results at N = 1 (configs 3, 4, 5, SURVEY 8f rows 1-3 and the host-memory path)
 # --------------------------------------------------------------------------------------
-def secondary_csr(dev, steps, warm_ms, verify):
+def secondary_csr(dev, steps, warm_ms, verify, cpu=False):
+    import numpy as np
     import torch
 
     import k2hash_amd
@@ -416,12 +466,21 @@ def secondary_csr(dev, steps, warm_ms, verify):
            "value": n * steps / wall, "unit": "key hashes/s", "roofline": roofline("csr", algo, kern, model, n)}
     if verify:
         res["verify"] = verify_chunks(h1, 0, _golden()["csr_8_256_64M"]["chunks"])
+    if cpu:  # the reference on the host cores over the first 16M keys of the same input
+        m = 1 << 24
+        host_off = off[:m + 1].cpu().numpy().view(np.uint64)
+        host_bytes = data[:int(host_off[-1])].cpu().numpy()
+        res["cpu_baseline"] = cpu_baseline_workload("csr", host_bytes, host_off, 0, 1 << 21, m,
+                                                    h1[:m].cpu().numpy())
+        res["gpu_over_cpu_cores"] = res["value"] / res["cpu_baseline"]["value"]
+        del host_off, host_bytes
     del off, data, h1
     torch.cuda.empty_cache()
     return res
 
 
-def secondary_fixed(name, dev, steps, warm_ms, verify, golden_name):
+def secondary_fixed(name, dev, steps, warm_ms, verify, golden_name, cpu=False):
+    import numpy as np
     import torch
 
     import k2hash_amd
@@ -441,6 +500,13 @@ def secondary_fixed(name, dev, steps, warm_ms, verify, golden_name):
     if verify:
         g = _golden()[golden_name]
         res["verify"] = verify_chunks(h1, 0, g.get("chunks") or [dict(first=0, count=g["n"], h1=g["h1"])])
+    if cpu:  # the reference on the host cores over a prefix of the same keys (1 GiB)
+        m = min(n, (1 << 30) // L)
+        host = keys[:m * L].cpu().numpy()
+        res["cpu_baseline"] = cpu_baseline_workload("fixed", host, None, L, max(1, m // 8), m,
+                                                    h1[:m].cpu().numpy())
+        res["gpu_over_cpu_cores"] = res["value"] / res["cpu_baseline"]["value"]
+        del host
     del keys, h1
     torch.cuda.empty_cache()
     return res
@@ -841,14 +907,21 @@ def main():
             torch.cuda.empty_cache()
             vf = not args.no_verify
             secondary = {
-                "csr": secondary_csr(dev, 20, 60.0, vf),
-                "fixed4096": secondary_fixed("fixed4096", dev, 20, 60.0, vf, "fixed4096_1M"),
+                "csr": secondary_csr(dev, 20, 60.0, vf, cpu=not args.no_cpu_baseline),
+                "fixed4096": secondary_fixed("fixed4096", dev, 20, 60.0, vf, "fixed4096_1M",
+                                             cpu=not args.no_cpu_baseline),
                 "fixed32_1g": secondary_fixed("fixed32_1g", dev, 10, 60.0, vf, "fixed32_1G"),
                 "fixed32_index": secondary_index(dev, 20, 60.0, vf),
                 "ralledata": secondary_ralledata(dev, 20, 60.0, vf),
                 "import": secondary_import(dev, 10, 60.0, vf),
                 "host": secondary_host(dev),
             }
+            cb = secondary["csr"].get("cpu_baseline")
+            if cb:  # the host path's CSR rate beside the reference on the box's cores (same key mix)
+                hc = secondary["host"]["csr_8M"]
+                hc["cpu_reference_cores"] = {"threads": cb["cores"]["threads"], "value": cb["cores"]["value"],
+                                             "key_gb_per_s": cb["cores"]["key_gb_per_s"]}
+                hc["host_path_over_cpu_cores"] = hc["value"] / cb["cores"]["value"]
         if not args.no_cpu_baseline:
             host = batch.synth_bytes(n * shape, dev).cpu().numpy()
             cpu = cpu_baseline(host, shape, n)

@@ -167,3 +167,78 @@ double cpu_bench_k2hbench(const char* so, int loops, int dcount, int threads, ui
   if (digest) *digest = d;
   return worst;
 }
+
+struct csr_job {
+  hash_fn h1, h2;
+  const uint8_t* bytes;
+  const uint64_t* off;
+  uint64_t first, count;
+  int passes, want_h2;
+  uint64_t digest;
+  pthread_barrier_t *ready, *go;
+};
+
+static void* csr_worker(void* a) {
+  struct csr_job* j = (struct csr_job*)a;
+  uint64_t d = 0;
+  pthread_barrier_wait(j->ready);
+  pthread_barrier_wait(j->go);
+  for (int p = 0; p < j->passes; ++p) {
+    uint64_t x = 0;
+    for (uint64_t i = j->first; i < j->first + j->count; ++i) {
+      const uint8_t* k = j->bytes + j->off[i];
+      const size_t len = (size_t)(j->off[i + 1] - j->off[i]);
+      x ^= j->h1(k, len);
+      if (j->want_h2) x ^= j->h2(k, len) * 3;
+    }
+    if (p == 0) d = x; /* digest of one pass (xor of h1 over the shard) */
+  }
+  j->digest = d;
+  return NULL;
+}
+
+/* CSR keys (bytes + n+1 offsets): the exact config-3 input, one contiguous shard of about
+ * equal BYTES per thread (cut on key boundaries).  Returns wall seconds from the release
+ * of the parked workers to the last join over `passes` passes; *digest = xor of h1 over
+ * the n keys (one pass). */
+double cpu_bench_csr(const char* so, const uint8_t* bytes, const uint64_t* off, uint64_t n, int threads, int passes,
+                     int want_h2, uint64_t* digest) {
+  hash_fn h1, h2;
+  if (resolve(so, &h1, &h2)) return -1.0;
+  if (threads < 1) threads = 1;
+  struct csr_job* jobs = (struct csr_job*)calloc((size_t)threads, sizeof *jobs);
+  pthread_t* th = (pthread_t*)calloc((size_t)threads, sizeof *th);
+  pthread_barrier_t ready, go;
+  pthread_barrier_init(&ready, NULL, (unsigned)threads + 1);
+  pthread_barrier_init(&go, NULL, (unsigned)threads + 1);
+  const uint64_t total = off[n] - off[0];
+  uint64_t a = 0;
+  for (int t = 0; t < threads; ++t) {
+    /* first key whose start is at or past the t+1-th byte quantile */
+    uint64_t want = off[0] + total / (uint64_t)threads * (uint64_t)(t + 1), lo = a, hi = n;
+    if (t + 1 == threads) lo = n;
+    while (lo < hi) {
+      uint64_t mid = lo + (hi - lo) / 2;
+      if (off[mid] < want) lo = mid + 1;
+      else hi = mid;
+    }
+    jobs[t] = (struct csr_job){h1, h2, bytes, off, a, lo - a, passes, want_h2, 0, &ready, &go};
+    a = lo;
+    pthread_create(&th[t], NULL, csr_worker, &jobs[t]);
+  }
+  pthread_barrier_wait(&ready);
+  double t0 = now();
+  pthread_barrier_wait(&go);
+  uint64_t d = 0;
+  for (int t = 0; t < threads; ++t) {
+    pthread_join(th[t], NULL);
+    d ^= jobs[t].digest;
+  }
+  double dt = now() - t0;
+  pthread_barrier_destroy(&ready);
+  pthread_barrier_destroy(&go);
+  free(jobs);
+  free(th);
+  if (digest) *digest = d;
+  return dt;
+}

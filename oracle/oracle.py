@@ -164,9 +164,15 @@ def cpubench():
     if not CPUBENCH_SO.exists():
         build()
     L = ctypes.CDLL(str(CPUBENCH_SO))
+    if not hasattr(L, "cpu_bench_csr"):  # built before the CSR harness existed
+        build()
+        L = ctypes.CDLL(str(CPUBENCH_SO))
     L.cpu_bench_fixed.restype = ctypes.c_double
     L.cpu_bench_fixed.argtypes = [ctypes.c_char_p, _p, _u64, _u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.POINTER(_u64)]
+    L.cpu_bench_csr.restype = ctypes.c_double
+    L.cpu_bench_csr.argtypes = [ctypes.c_char_p, _p, _p, _u64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                ctypes.POINTER(_u64)]
     L.cpu_bench_k2hbench.restype = ctypes.c_double
     L.cpu_bench_k2hbench.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                      ctypes.POINTER(_u64)]

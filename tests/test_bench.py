@@ -137,3 +137,25 @@ def test_bench_measures_the_baseline_metric_and_configs():
     assert bench.CONFIGS["csr"][1:3] == (1 << 26, (8, 256)) and "64M mixed-length keys 8" in base["configs"][2]
     assert bench.CONFIGS["fixed32_1g"][1] is None and bench.KEYS_1G == 1 << 30 and "1B 32B keys" in base["configs"][3]
     assert bench.CONFIGS["fixed4096"][1:3] == (1 << 20, 4096) and "4 KiB keys" in base["configs"][4]
+
+
+def test_cpu_baseline_workload_csr_and_fixed(oracle):
+    """The secondary configs' CPU legs (the reference's scalar hash over the
+    exact C3 / C5 inputs) on a small prefix: digests agree with the oracle's hashes."""
+    import numpy as np
+
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    off = oracle.gen_offsets(3000, 8, 256)
+    data = oracle.gen_bytes(int(off[-1]))
+    h1, _ = oracle.hash_csr(data, off)
+    r = bench.cpu_baseline_workload("csr", data, off.astype(np.uint64), 0, 500, 3000, h1.copy())
+    assert r["digest_matches_gpu"] is True and r["cores"]["keys"] == 3000 and r["single_thread"]["value"] > 0
+    keys = oracle.gen_bytes(4096 * 64)
+    f1, _ = oracle.hash_fixed(keys, 4096)
+    r = bench.cpu_baseline_workload("fixed", keys, None, 4096, 8, 64, f1.copy())
+    assert r["digest_matches_gpu"] is True and r["cores"]["key_bytes"] == 64 * 4096
+    bad = f1.copy()
+    bad[3] ^= 1
+    assert bench.cpu_baseline_workload("fixed", keys, None, 4096, 8, 64, bad)["digest_matches_gpu"] is False
