@@ -112,7 +112,7 @@ int k2h_amd_hash_csr_host(const void* bytes, const uint64_t* offsets, uint64_t n
  *   ckindex[i]    = h & collision_mask
  * i.e. &key_index_area[KIPtrArrayPos][KIArrayPos] (CVT_ABS_PKINDEX, lib/k2hshm.cc:50)
  * and &ckey_list[ckindex].  The table-state part of GetKIndex (walking cur_mask down
- * past unassigned K_INDEX entries, lib/k2hshm.cc:882-907) stays with the caller.
+ * past unassigned K_INDEX entries, lib/k2hshm.cc:882-907) is the *_table forms below.
  * kindex and ckindex may each be NULL; cur_mask must fit 58 bits when kindex is wanted.
  * The fused forms hash and index in one pass (the index costs no extra key read).
  * ------------------------------------------------------------------------- */
@@ -127,6 +127,35 @@ int k2h_amd_hash_fixed_index(const void* keys, uint64_t key_len, uint64_t n, uin
 int k2h_amd_hash_csr_index(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1, uint64_t* h2,
                            uint32_t flags, uint64_t cur_mask, uint64_t collision_mask, uint64_t* kindex,
                            uint64_t* ckindex, void* stream);
+
+/* Table-state forms: the K_INDEX that K2HShm::GetKIndex(hash, isMergeCurmask = false)
+ * returns (lib/k2hshm.cc:862-907) for a snapshot of the table's assigned flags: cur_mask
+ * walked down (cur_mask >>= 1 while > 0) until the entry GetKIndexPos gives for that mask
+ * has assign == KINDEX_ASSIGNED (lib/k2hstructure.h:40-41).  Without the side effect of
+ * the isMergeCurmask = true form (ArrangeToUpperKIndex): the caller rearranges.
+ *   table->assigned: device bitmap, one bit per K_INDEX entry of the mapped table, LSB
+ *     first in 32-bit words: entry KIArrayPos of key_index_area[KIPtrArrayPos] at bit
+ *     KIPtrArrayPos ? 2^(KIPtrArrayPos-1) + KIArrayPos : 0  (cur_mask + 1 bits).  NULL:
+ *     every entry assigned (= the stateless forms above).
+ *   kindex[i]: the entry reached, packed as above; when no probed entry is assigned, the
+ *     last probe's (mask 1), as the reference's loop leaves it; K2H_AMD_KINDEX_NONE when
+ *     cur_mask is 0 (the reference returns NULL).
+ *   found[i] (may be NULL): 1 when an assigned entry was reached, else 0. */
+#define K2H_AMD_KINDEX_NONE (~0ull)
+typedef struct k2h_amd_table {
+  uint64_t cur_mask;         /* K2HSHM cur_mask */
+  uint64_t collision_mask;   /* K2HSHM collision_mask */
+  const uint32_t* assigned;  /* device bitmap of assigned K_INDEX entries, or NULL */
+} k2h_amd_table;
+
+int k2h_amd_bucket_index_table(const uint64_t* h1, uint64_t n, const k2h_amd_table* table, uint64_t* kindex,
+                               uint64_t* ckindex, uint8_t* found, void* stream);
+int k2h_amd_hash_fixed_index_table(const void* keys, uint64_t key_len, uint64_t n, uint64_t* h1, uint64_t* h2,
+                                   uint32_t flags, const k2h_amd_table* table, uint64_t* kindex, uint64_t* ckindex,
+                                   uint8_t* found, void* stream);
+int k2h_amd_hash_csr_index_table(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1,
+                                 uint64_t* h2, uint32_t flags, const k2h_amd_table* table, uint64_t* kindex,
+                                 uint64_t* ckindex, uint8_t* found, void* stream);
 
 /* ---------------------------------------------------------------------------
  * 4. RALLEDATA producer (bulk direct-set input with precomputed hashes).

@@ -26,6 +26,14 @@ K2H_AMD_IMPORT_TSV, K2H_AMD_IMPORT_MDBM = 0, 1
 _u64 = ctypes.c_uint64
 _p = ctypes.c_void_p
 
+
+class Table(ctypes.Structure):
+    """k2h_amd_table (include/k2hash_amd.h section 3)."""
+    _fields_ = [("cur_mask", ctypes.c_uint64), ("collision_mask", ctypes.c_uint64), ("assigned", ctypes.c_void_p)]
+
+
+_tp = ctypes.POINTER(Table)
+
 # name -> (restype, argtypes); mirrors include/k2hash_amd.h
 SIGNATURES = {
     "k2h_hash": (_u64, [_p, ctypes.c_size_t]),
@@ -38,6 +46,9 @@ SIGNATURES = {
     "k2h_amd_bucket_index": (ctypes.c_int, [_p, _u64, _u64, _u64, _p, _p, _p]),
     "k2h_amd_hash_fixed_index": (ctypes.c_int, [_p, _u64, _u64, _p, _p, ctypes.c_uint32, _u64, _u64, _p, _p, _p]),
     "k2h_amd_hash_csr_index": (ctypes.c_int, [_p, _p, _u64, _p, _p, ctypes.c_uint32, _u64, _u64, _p, _p, _p]),
+    "k2h_amd_bucket_index_table": (ctypes.c_int, [_p, _u64, _tp, _p, _p, _p, _p]),
+    "k2h_amd_hash_fixed_index_table": (ctypes.c_int, [_p, _u64, _u64, _p, _p, ctypes.c_uint32, _tp, _p, _p, _p, _p]),
+    "k2h_amd_hash_csr_index_table": (ctypes.c_int, [_p, _p, _u64, _p, _p, ctypes.c_uint32, _tp, _p, _p, _p, _p]),
     "k2h_amd_ralledata_size": (_u64, [_u64, _u64, _u64, _u64, _u64]),
     "k2h_amd_build_ralledata": (ctypes.c_int, [_p, _p, _p, _p, _p, _p, _p, _p, _u64, _p, _p, ctypes.c_uint32, _p]),
     "k2h_amd_build_ralledata_host": (ctypes.c_int,

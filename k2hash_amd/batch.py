@@ -210,6 +210,115 @@ def hash_csr_index(data, offsets, cur_mask: int, collision_mask: int, second: bo
     return h1, h2, k, c
 
 
+# ----------------------------------------------------------------------------
+# Table-state bucket index (include/k2hash_amd.h section 3, *_table forms): the K_INDEX
+# K2HShm::GetKIndex(hash, false) reaches (lib/k2hshm.cc:862-907) for a snapshot of the
+# table's assigned flags.  `assigned`: int32 device tensor, the bitmap of assigned
+# K_INDEX entries (bit p ? 2^(p-1) + a : 0 for entry a of key_index_area[p]), or None
+# (every entry assigned).  Returns (kindex, ckindex, found) -- found is uint8.
+# ----------------------------------------------------------------------------
+KINDEX_NONE = (1 << 64) - 1
+
+
+def _table(torch, cur_mask: int, collision_mask: int, assigned, device):
+    if assigned is not None:
+        _check_dev(assigned, "assigned", torch.int32)
+        if assigned.device != device:
+            raise ValueError("assigned must be on the hashes' device")
+        need = (cur_mask + 1 + 31) // 32
+        if assigned.numel() < need:
+            raise ValueError(f"assigned must hold cur_mask + 1 bits ({need} int32 words), got {assigned.numel()}")
+    return _native.Table(cur_mask, collision_mask, assigned.data_ptr() if assigned is not None else None)
+
+
+def _table_outs(torch, n, device, kindex, ckindex, found, out):
+    if out is not None:
+        if len(out) != 3:
+            raise ValueError("out must be (kindex, ckindex, found)")
+        for t, name, dt in zip(out, ("kindex", "ckindex", "found"), (torch.int64, torch.int64, torch.uint8)):
+            if t is not None:
+                _check_dev(t, f"out {name}", dt)
+                if t.device != device or t.numel() != n:
+                    raise ValueError(f"out {name} must have {n} entries on {device}")
+        return out
+    return (torch.empty(n, dtype=torch.int64, device=device) if kindex else None,
+            torch.empty(n, dtype=torch.int64, device=device) if ckindex else None,
+            torch.empty(n, dtype=torch.uint8, device=device) if found else None)
+
+
+def _ptr_or_none(t):
+    return _dev_ptr(t) if t is not None else None
+
+
+def bucket_index_table(h1, cur_mask: int, collision_mask: int, assigned=None, kindex: bool = True,
+                       ckindex: bool = True, found: bool = True, out=None, stream=None):
+    """GetKIndex positions of hashes already in device memory, over a table snapshot."""
+    torch = _torch()
+    _check_dev(h1, "h1", torch.int64)
+    n = h1.numel()
+    tab = _table(torch, cur_mask, collision_mask, assigned, h1.device)
+    k, c, f = _table_outs(torch, n, h1.device, kindex, ckindex, found, out)
+    rc = _native.batch_lib().k2h_amd_bucket_index_table(_dev_ptr(h1), n, ctypes.byref(tab), _ptr_or_none(k),
+                                                         _ptr_or_none(c), _ptr_or_none(f), _stream_handle(stream))
+    _native.check(rc)
+    return k, c, f
+
+
+def hash_fixed_index_table(keys, key_len: int, cur_mask: int, collision_mask: int, assigned=None,
+                           second: bool = False, std_fnv: bool = False, stream=None):
+    """hash_fixed + the table-state bucket index in one pass: (h1, h2, kindex, ckindex, found)."""
+    torch = _torch()
+    _check_dev(keys, "keys", torch.uint8)
+    if key_len <= 0:
+        raise ValueError("key_len must be positive")
+    n = keys.numel() // key_len
+    tab = _table(torch, cur_mask, collision_mask, assigned, keys.device)
+    h1 = torch.empty(n, dtype=torch.int64, device=keys.device)
+    h2 = torch.empty(n, dtype=torch.int64, device=keys.device) if second else None
+    k, c, f = _table_outs(torch, n, keys.device, True, True, True, None)
+    rc = _native.batch_lib().k2h_amd_hash_fixed_index_table(
+        _dev_ptr(keys), key_len, n, _dev_ptr(h1), _ptr_or_none(h2), FLAG_STD_FNV if std_fnv else 0,
+        ctypes.byref(tab), _dev_ptr(k), _dev_ptr(c), _dev_ptr(f), _stream_handle(stream))
+    _native.check(rc)
+    return h1, h2, k, c, f
+
+
+def hash_csr_index_table(data, offsets, cur_mask: int, collision_mask: int, assigned=None, second: bool = False,
+                         std_fnv: bool = False, stream=None):
+    """hash_csr + the table-state bucket index in one pass: (h1, h2, kindex, ckindex, found)."""
+    torch = _torch()
+    _check_dev(data, "data", torch.uint8)
+    _check_dev(offsets, "offsets", torch.int64)
+    n = offsets.numel() - 1
+    if n < 0:
+        raise ValueError("offsets must have n+1 entries")
+    tab = _table(torch, cur_mask, collision_mask, assigned, data.device)
+    h1 = torch.empty(n, dtype=torch.int64, device=data.device)
+    h2 = torch.empty(n, dtype=torch.int64, device=data.device) if second else None
+    k, c, f = _table_outs(torch, n, data.device, True, True, True, None)
+    base = _dev_ptr(data) if data.numel() > 0 else ctypes.c_void_p(data.data_ptr() or 1)
+    rc = _native.batch_lib().k2h_amd_hash_csr_index_table(
+        base, _dev_ptr(offsets), n, _dev_ptr(h1), _ptr_or_none(h2), FLAG_STD_FNV if std_fnv else 0,
+        ctypes.byref(tab), _dev_ptr(k), _dev_ptr(c), _dev_ptr(f), _stream_handle(stream))
+    _native.check(rc)
+    return h1, h2, k, c, f
+
+
+def expanded_table_bitmap(cur_mask: int, frac_top: float, seed: int = 0):
+    """Assigned-entry bitmap (numpy uint32) of a table just expanded to `cur_mask`: every
+    entry below the top area assigned, a fraction `frac_top` of the top area's entries
+    (those ArrangeToUpperKIndex has already split) assigned.  Test / bench helper."""
+    bits = cur_mask + 1
+    flags = np.ones(bits, dtype=bool)
+    top = (cur_mask + 1) // 2
+    if cur_mask:
+        rng = np.random.default_rng(seed)
+        flags[top:] = rng.random(bits - top) < frac_top
+    words = np.zeros((bits + 31) // 32 * 32, dtype=bool)
+    words[:bits] = flags
+    return np.packbits(words.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").astype(np.uint32).reshape(-1)
+
+
 def _np_ptr(a: np.ndarray) -> ctypes.c_void_p:
     return ctypes.c_void_p(a.ctypes.data)
 

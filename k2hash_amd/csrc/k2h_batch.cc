@@ -352,6 +352,64 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_index(const void* by
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_csr (index)", e);
 }
 
+__attribute__((visibility("default"))) int k2h_amd_bucket_index_table(const uint64_t* h1, uint64_t n,
+                                                                      const k2h_amd_table* table, uint64_t* kindex,
+                                                                      uint64_t* ckindex, uint8_t* found, void* stream) {
+  if (!table) return fail(K2H_AMD_EINVAL, "table is NULL");
+  if (n == 0 || (!kindex && !ckindex && !found)) return K2H_AMD_OK;
+  if (!h1) return fail(K2H_AMD_EINVAL, "h1 is NULL");
+  k2h::BucketParams bp;
+  int rc = bucket_params(table->cur_mask, table->collision_mask, kindex, ckindex, bp);
+  if (rc) return rc;
+  bp.assigned = table->assigned;
+  bp.found = table->assigned ? found : nullptr;
+  if (found && !table->assigned) {  // every entry assigned: found is all ones unless cur_mask is 0
+    hipError_t e = hipMemsetAsync(found, table->cur_mask ? 1 : 0, n, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "found fill", e);
+  }
+  hipError_t e = k2h::launch_bucket_index(h1, n, bp, (hipStream_t)stream);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_bucket_index (table)", e);
+}
+
+__attribute__((visibility("default"))) int k2h_amd_hash_fixed_index_table(
+    const void* keys, uint64_t key_len, uint64_t n, uint64_t* h1, uint64_t* h2, uint32_t flags,
+    const k2h_amd_table* table, uint64_t* kindex, uint64_t* ckindex, uint8_t* found, void* stream) {
+  if (!table) return fail(K2H_AMD_EINVAL, "table is NULL");
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1) return fail(K2H_AMD_EINVAL, "h1 is NULL");
+  if (key_len && n > UINT64_MAX / key_len) return fail(K2H_AMD_EINVAL, "n * key_len overflows");
+  k2h::BucketParams bp;
+  int rc = bucket_params(table->cur_mask, table->collision_mask, kindex, ckindex, bp);
+  if (rc) return rc;
+  bp.assigned = table->assigned;
+  bp.found = table->assigned ? found : nullptr;
+  if (found && !table->assigned) {
+    hipError_t e = hipMemsetAsync(found, table->cur_mask ? 1 : 0, n, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "found fill", e);
+  }
+  hipError_t e = k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_fixed (table index)", e);
+}
+
+__attribute__((visibility("default"))) int k2h_amd_hash_csr_index_table(
+    const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t* h1, uint64_t* h2, uint32_t flags,
+    const k2h_amd_table* table, uint64_t* kindex, uint64_t* ckindex, uint8_t* found, void* stream) {
+  if (!table) return fail(K2H_AMD_EINVAL, "table is NULL");
+  if (n == 0) return K2H_AMD_OK;
+  if (!h1 || !offsets) return fail(K2H_AMD_EINVAL, "h1/offsets is NULL");
+  k2h::BucketParams bp;
+  int rc = bucket_params(table->cur_mask, table->collision_mask, kindex, ckindex, bp);
+  if (rc) return rc;
+  bp.assigned = table->assigned;
+  bp.found = table->assigned ? found : nullptr;
+  if (found && !table->assigned) {
+    hipError_t e = hipMemsetAsync(found, table->cur_mask ? 1 : 0, n, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "found fill", e);
+  }
+  hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
+  return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_csr (table index)", e);
+}
+
 __attribute__((visibility("default"))) int k2h_amd_hash_fixed_host(const void* keys, uint64_t key_len, uint64_t n,
                                                                    uint64_t* h1, uint64_t* h2, uint32_t flags,
                                                                    int device) {

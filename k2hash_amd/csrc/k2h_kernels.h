@@ -21,12 +21,20 @@ constexpr uint64_t kSeedStdValue = 2166136261ULL;                  // libstdc++ 
 //   KIArrayPos    = shifted & MakeMask(KIPtrArrayPos - 1)   (MakeMask(0) = 0)
 // kindex[i] packs KIPtrArrayPos << 58 | KIArrayPos (bitlen(cur_mask) <= 58 checked by the
 // ABI); ckindex[i] = hash & collision_mask.  Either output may be null.
+// Table state (assigned != null): K2HShm::GetKIndex(hash, false) (lib/k2hshm.cc:882-907)
+// -- cur_mask walked down (>>= 1) until the K_INDEX at the masked shifted hash is
+// assigned; `assigned` has one bit per K_INDEX entry, entry (p, a) at bit p ? 2^(p-1)+a : 0,
+// which is exactly the masked shifted hash v = (hash >> cshift) & m (p = bitlen(v),
+// a = v without its top bit).  No assigned entry: the mask-1 probe (what the loop leaves);
+// cur_mask 0: kindex = all ones (NULL).  found[i] = 1 when an assigned entry was reached.
 struct BucketParams {
   uint64_t cur_mask = 0;
   uint64_t collision_mask = 0;
   uint32_t cshift = 0;
   uint64_t* kindex = nullptr;
   uint64_t* ckindex = nullptr;
+  const uint32_t* assigned = nullptr;
+  uint8_t* found = nullptr;
 };
 constexpr int kKindexPosShift = 58;
 
@@ -36,7 +44,26 @@ constexpr int kKindexPosShift = 58;
 // plain stores so that L2 merges the partial lines before they reach HBM.
 template <bool NT = true>
 __device__ __forceinline__ void bucket_emit(const BucketParams& bp, uint64_t i, uint64_t h) {
-  if (bp.kindex) {
+  if (bp.assigned) {  // table state: GetKIndex's walk over the assigned K_INDEX entries
+    const uint64_t shifted = h >> (bp.cshift & 63u);
+    uint64_t tmp = 0;
+    bool hit = false;
+    for (uint64_t m = bp.cur_mask; m; m >>= 1) {
+      tmp = shifted & m;
+      if ((bp.assigned[tmp >> 5] >> (tmp & 31u)) & 1u) {
+        hit = true;
+        break;
+      }
+    }
+    if (bp.kindex) {
+      const uint64_t pos = tmp ? 64u - (uint64_t)__clzll((long long)tmp) : 0u;
+      const uint64_t arr = pos ? tmp & ((1ull << (pos - 1)) - 1ull) : 0u;
+      const uint64_t v = bp.cur_mask ? (pos << kKindexPosShift) | arr : ~0ull;
+      if constexpr (NT) __builtin_nontemporal_store(v, bp.kindex + i);
+      else bp.kindex[i] = v;
+    }
+    if (bp.found) bp.found[i] = hit;
+  } else if (bp.kindex) {
     uint64_t shifted = h >> (bp.cshift & 63u);
     uint64_t tmp = shifted & bp.cur_mask;
     uint64_t pos = tmp ? 64u - (uint64_t)__clzll((long long)tmp) : 0u;

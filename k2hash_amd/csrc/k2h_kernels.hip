@@ -148,7 +148,7 @@ __global__ __launch_bounds__(64) void fnv_fixed32_kpt_kernel(const uint4* __rest
 }
 
 hipError_t launch_bucket_index(const uint64_t* h1, uint64_t n, const BucketParams& bp, hipStream_t stream) {
-  if (n == 0 || !(bp.kindex || bp.ckindex)) return hipSuccess;
+  if (n == 0 || !(bp.kindex || bp.ckindex || bp.found)) return hipSuccess;
   bucket_index_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n, bp);
   return hipGetLastError();
 }
@@ -162,7 +162,7 @@ hipError_t launch_bucket_index(const uint64_t* h1, uint64_t n, const BucketParam
 hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,
                         hipStream_t stream, const BucketParams* bp) {
   if (n == 0) return hipSuccess;
-  const bool epi = bp && (bp->kindex || bp->ckindex);
+  const bool epi = bp && (bp->kindex || bp->ckindex || bp->found);
   if (!keys || key_len == 0) {
     fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n);
     if (h2) fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h2, n);
@@ -199,7 +199,7 @@ hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t
 hipError_t launch_csr(const void* bytes, const uint64_t* offsets, uint64_t n, uint64_t seed, uint64_t* h1,
                       uint64_t* h2, hipStream_t stream, const BucketParams* bp) {
   if (n == 0) return hipSuccess;
-  const bool epi = bp && (bp->kindex || bp->ckindex);
+  const bool epi = bp && (bp->kindex || bp->ckindex || bp->found);
   if (!bytes) {
     fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h1, n);
     if (h2) fill_zero_kernel<<<grid_for(n), 256, 0, stream>>>(h2, n);

@@ -181,6 +181,50 @@ void oracle_bucket_index(const uint64_t* h, size_t n, uint64_t cur_mask, uint64_
   }
 }
 
+/* lib/k2hshm.cc:862-907 K2HShm::GetKIndex(hash, isMergeCurmask = false): walk cur_mask
+ * down (cur_mask >>= 1 while > 0), computing GetKIndexPos with each mask (the
+ * pCurMask form, lib/k2hshm.cc:810-833), and stop at the first K_INDEX whose `assign` is
+ * KINDEX_ASSIGNED (lib/k2hstructure.h:40-41, 160-165); if none is, the pointer of the
+ * last probe (mask 1) is what the loop leaves in pKindex; with cur_mask 0 the loop does
+ * not run and the result is NULL.  The isMergeCurmask = true form also rearranges the
+ * table (ArrangeToUpperKIndex), a write this batch form does not model.
+ *
+ * Table state: `assigned` is a bitmap with one bit per K_INDEX entry of the mapped
+ * table, entry KIArrayPos of key_index_area[KIPtrArrayPos] (CVT_ABS_PKINDEX,
+ * lib/k2hshm.cc:50) at bit  KIPtrArrayPos ? 2^(KIPtrArrayPos-1) + KIArrayPos : 0
+ * (area p holds 2^(p-1) entries, area 0 one: the table's cur_mask + 1 entries in area
+ * order).  Returns 1 (assigned entry reached), 0 (walk ended on an unassigned entry),
+ * -1 (cur_mask 0: NULL).  Parity of this walk is unpinned: K2HShm needs the mapped table
+ * and libfullock, so the reference's GetKIndex is not executed here; only its stateless
+ * part (GetKIndexPos) is pinned, by the dsave fixture and the key_index_area table. */
+int oracle_get_kindex(uint64_t hash, uint64_t cur_mask, uint64_t collision_mask, const uint32_t* assigned,
+                      uint64_t* kiptr_pos, uint64_t* kiarray_pos) {
+  int found = -1;
+  for (uint64_t m = cur_mask; 0 < m; m = m >> 1) {
+    uint64_t p, a, c;
+    oracle_kindex_pos(hash, m, collision_mask, &p, &a, &c);
+    *kiptr_pos = p;
+    *kiarray_pos = a;
+    const uint64_t bit = p ? (1ull << (p - 1)) + a : 0;
+    if ((assigned[bit >> 5] >> (bit & 31)) & 1u) return 1;
+    found = 0;
+  }
+  return found;
+}
+
+/* Batch form: kindex packed as above, K2H_AMD_KINDEX_NONE (all ones) for NULL; found[i]
+ * = 1 when an assigned entry was reached. */
+void oracle_bucket_index_table(const uint64_t* h, size_t n, uint64_t cur_mask, uint64_t collision_mask,
+                               const uint32_t* assigned, uint64_t* kindex, uint64_t* ckindex, uint8_t* found) {
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t p = 0, a = 0;
+    const int r = oracle_get_kindex(h[i], cur_mask, collision_mask, assigned, &p, &a);
+    if (kindex) kindex[i] = r < 0 ? ~0ull : (p << 58) | a;
+    if (ckindex) ckindex[i] = h[i] & collision_mask;
+    if (found) found[i] = r > 0;
+  }
+}
+
 /* ---------------------------------------------------------------------------
  * RALLEDATA producer, restated: one packed blob per record,
  * laid out as K2HShm::GetElementToBinary does (lib/k2hshmdirect.cc:59-88) on the

@@ -179,6 +179,23 @@ def cpubench():
     return L
 
 
+def bucket_index_table(h, cur_mask: int, collision_mask: int, assigned):
+    """GetKIndex(hash, false) over a table snapshot (oracle_bucket_index_table): returns
+    (kindex, ckindex, found) numpy arrays; `assigned` is the uint32 bitmap of K_INDEX
+    entries (fnv_oracle.c)."""
+    h = np.ascontiguousarray(h, dtype=np.uint64)
+    assigned = np.ascontiguousarray(assigned, dtype=np.uint32)
+    n = h.size
+    k = np.empty(n, np.uint64)
+    c = np.empty(n, np.uint64)
+    f = np.empty(n, np.uint8)
+    L = lib()
+    L.oracle_bucket_index_table.restype = None
+    L.oracle_bucket_index_table.argtypes = [_p, _sz, _u64, _u64, _p, _p, _p, _p]
+    L.oracle_bucket_index_table(_ptr(h), n, cur_mask, collision_mask, _ptr(assigned), _ptr(k), _ptr(c), _ptr(f))
+    return k, c, f
+
+
 def kindex_pos(h: int, cur_mask: int, collision_mask: int) -> tuple[int, int, int]:
     """(KIPtrArrayPos, KIArrayPos, ckindex) of one hash (lib/k2hshm.cc:810-833, 1093)."""
     p, a, c = _u64(), _u64(), _u64()

@@ -210,3 +210,132 @@ def test_fused_full_size_vs_oracle(cuda, oracle, digests, cfgname, cur, cm):
     rk, rc = oracle.bucket_index(hh, cur, cm)
     assert np.array_equal(k.cpu().numpy().view(np.uint64), rk)
     assert np.array_equal(c.cpu().numpy().view(np.uint64), rc)
+
+
+# ---------------------------------------------------------------------------
+# Table state: K2HShm::GetKIndex(hash, isMergeCurmask = false) over a snapshot of the
+# assigned K_INDEX entries (lib/k2hshm.cc:862-907).  Parity is UNPINNED beyond the
+# restatement: K2HShm::GetKIndex needs the mapped table and libfullock, so the reference
+# function is not executed; the oracle's walk (oracle/fnv_oracle.c oracle_get_kindex) is
+# checked here against an independent Python restatement, and with every entry assigned
+# it must reduce to the pinned stateless GetKIndexPos.
+# ---------------------------------------------------------------------------
+def _py_get_kindex(h, cur_mask, cmask, flags):
+    """lib/k2hshm.cc:882-907 in Python: flags[(p, a)] = assigned."""
+    res, found = None, -1
+    m = cur_mask
+    while m > 0:
+        shifted = h >> (cmask.bit_length() % 64)  # GetMaskBitCount, shift count mod 64
+        tmp = shifted & m
+        p = tmp.bit_length()
+        a = shifted & ((1 << (p - 1)) - 1 if p else 0)
+        res = (p, a)
+        if flags(p, a):
+            return res, 1
+        found = 0
+        m >>= 1
+    return res, found
+
+
+def _bitmap_from(flags_fn, cur_mask):
+    bits = np.zeros(((cur_mask + 1 + 31) // 32) * 32, dtype=np.uint8)
+    for v in range(cur_mask + 1):
+        p = v.bit_length()
+        a = v - (1 << (p - 1)) if p else 0
+        bits[v] = flags_fn(p, a)
+    return np.packbits(bits.reshape(-1, 32)[:, ::-1], axis=1).view(">u4").astype(np.uint32).reshape(-1)
+
+
+@pytest.mark.parametrize("cur_mask,cmask", [(0x3, 0x3), (0xFF, 0xF), (0x1, 0x0), (0x0, 0xF), (0x3FF, 0x0),
+                                            ((1 << 12) - 1, (1 << 8) - 1)])
+def test_get_kindex_restatement(oracle, cur_mask, cmask):
+    rng = np.random.default_rng(cur_mask ^ cmask)
+    h = rng.integers(0, 2**63, size=3000, dtype=np.int64).view(np.uint64) * np.uint64(2) + np.uint64(1)
+    for density in (0.0, 0.3, 0.9, 1.0):
+        table = {}
+
+        def flags(p, a, _d=density):
+            if (p, a) not in table:
+                table[(p, a)] = bool(rng.random() < _d)
+            return table[(p, a)]
+        bm = _bitmap_from(flags, cur_mask)
+        k, c, f = oracle.bucket_index_table(h, cur_mask, cmask, bm)
+        for i in range(0, 3000, 7):
+            (res, fnd) = _py_get_kindex(int(h[i]), cur_mask, cmask, lambda p, a: table[(p, a)])
+            if fnd < 0:
+                assert int(k[i]) == (1 << 64) - 1 and f[i] == 0
+            else:
+                assert (int(k[i]) >> 58, int(k[i]) & ((1 << 58) - 1)) == res and f[i] == fnd
+            assert int(c[i]) == int(h[i]) & cmask
+    # every entry assigned: GetKIndex == GetKIndexPos (the pinned stateless part)
+    full = _bitmap_from(lambda p, a: True, cur_mask)
+    k, c, f = oracle.bucket_index_table(h, cur_mask, cmask, full)
+    ks, cs = oracle.bucket_index(h, cur_mask, cmask)
+    if cur_mask:
+        assert np.array_equal(k, ks) and np.array_equal(c, cs) and f.all()
+
+
+def test_expanded_table_bitmap_layout():
+    bm = batch.expanded_table_bitmap(0xFF, 0.5, seed=3)
+    assert bm.dtype == np.uint32 and bm.size == 8
+    bits = np.unpackbits(bm.astype(">u4").view(np.uint8).reshape(-1, 4), axis=1).reshape(-1, 32)[:, ::-1].reshape(-1)
+    assert bits[:128].all() and 0 < bits[128:].sum() < 128
+
+
+# ------------------------------------------------------------------------- GPU
+TABLES = [(0xFF, 0xF, 0.5), ((1 << 20) - 1, 0xF, 0.3), ((1 << 16) - 1, 0x0, 0.0), (0x3, 0x3, 0.9),
+          ((1 << 24) - 1, (1 << 4) - 1, 1.0), (0x0, 0xF, 1.0), (0x1, 0x0, 0.0)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cur_mask,cmask,frac", TABLES)
+def test_table_index_gpu_vs_oracle(cuda, oracle, cur_mask, cmask, frac):
+    """Standalone and fused (fixed 32 B, CSR) table-state index vs the oracle's GetKIndex
+    walk, on tables just expanded to cur_mask (top area partly arranged) and on random
+    per-entry bitmaps."""
+    import torch
+    n = 200003
+    data = oracle.gen_bytes(32 * n, byte_off=99)
+    r1, _ = oracle.hash_fixed(data, 32)
+    bms = [batch.expanded_table_bitmap(cur_mask, frac, seed=7)]
+    rng = np.random.default_rng(cur_mask)
+    bms.append(rng.integers(0, 2**32, size=(cur_mask + 1 + 31) // 32, dtype=np.uint64).astype(np.uint32))
+    keys = torch.from_numpy(data).to(cuda)
+    h1 = torch.from_numpy(r1.view(np.int64).copy()).to(cuda)
+    off = oracle.gen_offsets(20011, 0, 300)
+    cdata = oracle.gen_bytes(int(off[-1]))
+    c1, _ = oracle.hash_csr(cdata, off)
+    for bm in bms:
+        ok, oc, of = oracle.bucket_index_table(r1, cur_mask, cmask, bm)
+        assigned = torch.from_numpy(bm.view(np.int32).copy()).to(cuda)
+        k, c, f = batch.bucket_index_table(h1, cur_mask, cmask, assigned)
+        g1, _, gk, gc, gf = batch.hash_fixed_index_table(keys, 32, cur_mask, cmask, assigned)
+        torch.cuda.synchronize()
+        for kk, cc, ff in ((k, c, f), (gk, gc, gf)):
+            assert np.array_equal(kk.cpu().numpy().view(np.uint64), ok)
+            assert np.array_equal(cc.cpu().numpy().view(np.uint64), oc)
+            assert np.array_equal(ff.cpu().numpy(), of)
+        assert np.array_equal(g1.cpu().numpy().view(np.uint64), r1)
+        ck, cc_, cf = oracle.bucket_index_table(c1, cur_mask, cmask, bm)
+        x1, x2, xk, xc, xf = batch.hash_csr_index_table(torch.from_numpy(cdata).to(cuda),
+                                                        torch.from_numpy(off.astype(np.int64)).to(cuda),
+                                                        cur_mask, cmask, assigned, second=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(x1.cpu().numpy().view(np.uint64), c1)
+        assert np.array_equal(xk.cpu().numpy().view(np.uint64), ck)
+        assert np.array_equal(xc.cpu().numpy().view(np.uint64), cc_)
+        assert np.array_equal(xf.cpu().numpy(), cf)
+
+
+@pytest.mark.gpu
+def test_table_index_null_bitmap_is_stateless(cuda, oracle):
+    """assigned = NULL: every entry assigned, so the table form equals the stateless one."""
+    import torch
+    h = oracle.gen_bytes(8 * 50000).view(np.uint64)
+    th = torch.from_numpy(h.view(np.int64).copy()).to(cuda)
+    k, c, f = batch.bucket_index_table(th, 0xFFFF, 0xF, None)
+    ks, cs = batch.bucket_index(th, 0xFFFF, 0xF)
+    torch.cuda.synchronize()
+    assert torch.equal(k, ks) and torch.equal(c, cs) and bool((f == 1).all())
+    with pytest.raises(ValueError):  # bitmap shorter than cur_mask + 1 bits
+        batch.bucket_index_table(th, 0xFFFF, 0xF, torch.zeros(100, dtype=torch.int32, device=cuda))
