@@ -136,6 +136,55 @@ void oracle_digest(const uint64_t* h, size_t n, uint64_t first_index, uint64_t o
 }
 
 /* ---------------------------------------------------------------------------
+ * The exact split of one key's FNV-1a chain at byte m (the algebra a
+ * two-lane hash of one long key would use).  Per byte b with s = sext(b) (lib/k2hashfunc.cc
+ * :53-56) and v = h mod 256, w = v ^ b:
+ *   h ^ s = +h + (w - v)          for b <  0x80   (only the low byte changes)
+ *   h ^ s = -h + (v + w - 256)    for b >= 0x80   (~h = -h - 1 above the low byte)
+ * so h' = P (sigma h + d) with sigma = +-1 and d depending on (v, b) only, and the low byte
+ * runs its own chain v' = 0xB3 (v ^ b) mod 256 (P mod 256 = 0xB3).  Over bytes [m, N):
+ *   h_N = K (P^(N-m) h_m + E),  K = prod sigma,  E_{n+1} = P (E_n + K_{n+1} d_n), E_m = 0
+ * so a second lane that knows v_m (the 8-bit chain over [0, m)) computes (K, E) while the
+ * first lane computes h_m, and h_N follows from one multiply-add.
+ * ------------------------------------------------------------------------- */
+static uint64_t fnv_pow(uint64_t b, uint64_t e) {
+  uint64_t r = 1;
+  for (; e; e >>= 1, b *= b)
+    if (e & 1) r *= b;
+  return r;
+}
+
+uint64_t oracle_fnv_split(const uint8_t* p, size_t len, size_t m, uint64_t seed) {
+  const uint64_t P = 1099511628211ULL;
+  /* lane A: the plain chain over [0, m) */
+  uint64_t hm = seed;
+  for (size_t i = 0; i < m; ++i) hm = (hm ^ (uint64_t)(int64_t)(signed char)p[i]) * P;
+  /* lane B: the low byte over [0, m), then (K, E) over [m, len) */
+  uint32_t v = (uint32_t)(seed & 0xFF);
+  for (size_t i = 0; i < m; ++i) v = (0xB3u * (v ^ p[i])) & 0xFFu;
+  int64_t K = 1;
+  uint64_t E = 0;
+  for (size_t i = m; i < len; ++i) {
+    const uint32_t w = v ^ p[i];
+    const int neg = p[i] >= 0x80;
+    const int64_t d = neg ? (int64_t)v + (int64_t)w - 256 : (int64_t)w - (int64_t)v;
+    if (neg) K = -K;
+    E = P * (E + (uint64_t)(K * d));
+    v = (0xB3u * w) & 0xFFu;
+  }
+  const uint64_t r = fnv_pow(P, (uint64_t)(len - m)) * hm + E;
+  return K > 0 ? r : (uint64_t)0 - r;
+}
+
+/* Number of split points m in [0, len] where the split disagrees with the direct chain. */
+size_t oracle_fnv_split_mismatches(const uint8_t* p, size_t len, uint64_t seed) {
+  size_t bad = 0;
+  for (size_t m = 0; m <= len; ++m)
+    if (oracle_fnv_split(p, len, m, seed) != oracle_fnv(p, len, seed)) ++bad;
+  return bad;
+}
+
+/* ---------------------------------------------------------------------------
  * Bucket index: the stateless part of K2HShm::GetKIndexPos and
  * the collision slot of K2HShm::GetCKIndex, restated loop for loop.  The reference
  * functions are K2HShm members needing the mapped table and libfullock, so they are

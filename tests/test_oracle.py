@@ -147,3 +147,26 @@ def test_against_reference_std_fnv(oracle):
         k = bytes(rng.getrandbits(8) for _ in range(n))
         assert oracle.k2h_hash(k, 1) == ref.k2h_hash(k)
         assert oracle.k2h_second_hash(k, 1) == ref.k2h_second_hash(k)
+
+
+def test_fnv_split_every_point(oracle):
+    """The two-lane split of one key's chain (oracle_fnv_split): the
+    low-byte chain v' = 0xB3 (v ^ b) plus the signed affine accumulation reproduce the
+    direct chain at EVERY split point of a 4 KiB key -- the SURVEY vector
+    b[i] = (i*131+7) & 0xFF and random keys full of bytes >= 0x80 -- for both seeds."""
+    import ctypes
+
+    L = oracle.lib()
+    L.oracle_fnv_split_mismatches.restype = ctypes.c_size_t
+    L.oracle_fnv_split_mismatches.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
+    L.oracle_fnv_split.restype = ctypes.c_uint64
+    L.oracle_fnv_split.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64]
+    keys = [np.array([(i * 131 + 7) & 0xFF for i in range(4096)], np.uint8),
+            np.random.default_rng(11).integers(0, 256, 4096, dtype=np.uint8),
+            np.full(4096, 0xFF, np.uint8), np.full(300, 0x80, np.uint8)]
+    keys += [np.random.default_rng(k).integers(0x70, 0x90, k, dtype=np.uint8) for k in range(0, 70)]
+    for k in keys:
+        for seed in (14695981039346656037, 2166136261):
+            assert L.oracle_fnv_split_mismatches(k.ctypes.data, k.size, seed) == 0, (k.size, seed)
+    k = keys[0]
+    assert L.oracle_fnv_split(k.ctypes.data, 4096, 2048, 14695981039346656037) == 0x4dbdf6ea6a33a325  # SURVEY 8a

@@ -1,0 +1,110 @@
+#!/usr/bin/env python3
+"""Round-3 lab A/B: interleaved timing of tools/lab/libk2hash_lab.so variants against the
+product launch, each result digest-checked against the reference first.
+
+  python tools/lab_ab.py lines --variants 0:0 1:8 1:10 [--reps 5 --launches 20]
+      config 5 (1M x 4 KiB): variant:waves_per_cu
+  python tools/lab_ab.py csr --variants 0 1 2
+      config 3 (64M CSR keys)
+
+Prints one JSON object (per-variant median / min launch time in microseconds)."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402  (digest helpers)
+
+_p, _u64 = ctypes.c_void_p, ctypes.c_uint64
+
+
+def lab_lib():
+    lib = ctypes.CDLL(str(ROOT / "tools" / "lab" / "libk2hash_lab.so"))
+    if hasattr(lib, "k2h_lab_lines"):
+        lib.k2h_lab_lines.restype = ctypes.c_int
+        lib.k2h_lab_lines.argtypes = [ctypes.c_int, _p, _u64, _u64, _p, _p, ctypes.c_int, _p]
+    if hasattr(lib, "k2h_lab_csr"):
+        lib.k2h_lab_csr.restype = ctypes.c_int
+        lib.k2h_lab_csr.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+    return lib
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("config", choices=["lines", "csr"])
+    ap.add_argument("--variants", nargs="+", required=True)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--warm-ms", type=float, default=200.0)
+    args = ap.parse_args()
+
+    import torch
+
+    from k2hash_amd import batch
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    lib = lab_lib()
+    stream = torch.cuda.current_stream()
+    sh = ctypes.c_void_p(stream.cuda_stream)
+    gold = bench._golden()
+    if args.config == "lines":
+        n, L = 1 << 20, 4096
+        keys = batch.synth_bytes(n * L, dev)
+        h1 = torch.empty(n, dtype=torch.int64, device=dev)
+        g = gold["fixed4096_1M"]
+        chunks = g.get("chunks") or [dict(first=0, count=g["n"], h1=g["h1"])]
+
+        def launch(v):
+            var, wpc = (int(x) for x in v.split(":"))
+            rc = lib.k2h_lab_lines(var, ctypes.c_void_p(keys.data_ptr()), L, n, ctypes.c_void_p(h1.data_ptr()),
+                                   None, wpc, sh)
+            assert rc == 0, rc
+    else:
+        n = 1 << 26
+        off = batch.synth_offsets(n, dev, 8, 256)
+        data = batch.synth_bytes(int(off[-1].item()), dev)
+        h1 = torch.empty(n, dtype=torch.int64, device=dev)
+        chunks = gold["csr_8_256_64M"]["chunks"]
+
+        def launch(v):
+            rc = lib.k2h_lab_csr(int(v), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
+                                 ctypes.c_void_p(h1.data_ptr()), None, sh)
+            assert rc == 0, rc
+
+    res = {}
+    for v in args.variants:  # parity first
+        h1.zero_()
+        launch(v)
+        torch.cuda.synchronize()
+        res[v] = {"verify": bench.verify_chunks(h1, 0, chunks)}
+    import time
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < args.warm_ms:
+        for v in args.variants:
+            launch(v)
+        torch.cuda.synchronize()
+    times = {v: [] for v in args.variants}
+    for _ in range(args.reps):
+        for v in args.variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(args.launches):
+                launch(v)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) * 1e3 / args.launches)
+    for v in args.variants:
+        res[v].update({"median_us": statistics.median(times[v]), "min_us": min(times[v]), "all_us": times[v]})
+    print(json.dumps({"config": args.config, "n": n, "results": res}))
+
+
+if __name__ == "__main__":
+    main()
