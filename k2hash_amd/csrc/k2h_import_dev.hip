@@ -266,30 +266,31 @@ __global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* 
 unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
 
 // ---------------------------------------------------------------------------
-// TSV as the getline loop's own machine (round 2).  ConvertfromTsv
-// (tests/k2himport.cc:78-86) alternates getline(key, '\t') and getline(value): mode K
-// reads a key up to its TAB (newlines included), mode V a value up to its newline (TABs
-// included).  A record ends at every newline read in mode V, and one more at EOF if the
-// file stops in mode V (the value getline hits EOF after the key's TAB); a key getline
-// that hits EOF drops its bytes.  Set stores C strings (lib/k2hshm.cc:2081-2083), so a
-// field is cut at its first NUL: a NUL is its field's first iff the last NUL before it
-// lies before the field's start.  A span of bytes therefore acts on the state (mode,
-// record index, field start, last NUL) as a small function: per entry mode, the exit
-// mode, the record ends passed and the last field boundary (a TAB read in K, a newline
-// read in V); plus its last NUL.  These functions compose associatively (positions only
-// grow, so "last" combines with max), so each 16 KiB block gets its entry state from a
-// device scan of block functions and each thread from a block scan of 3-word functions
-// of its 128 bytes.  The thread then walks its bytes' events and writes every field at
-// its end event -- key (off, len) at the key's first NUL or else its TAB, value (off,
-// len) at the value's first NUL or else its newline (or EOF) -- and lists the keys that
-// end in its span; the block hashes its list from LDS.  The file is read twice (pass A:
-// block functions; pass B: the walk), and only the 32-byte records and the hashes are
-// written: no per-line arrays.
+// TSV as the getline loop's own machine.  ConvertfromTsv (tests/k2himport.cc:78-86)
+// alternates getline(key, '\t') and getline(value): mode K reads a key up to its TAB
+// (newlines included), mode V a value up to its newline (TABs included).  A record ends
+// at every newline read in mode V, and one more at EOF if the file stops in mode V (the
+// value getline hits EOF after the key's TAB); a key getline that hits EOF drops its
+// bytes.  Set stores C strings (lib/k2hshm.cc:2081-2083), so a field is cut at its first
+// NUL: a NUL is its field's first iff the last NUL before it lies before the field's
+// start.  A span of bytes therefore acts on the state (mode, record index, field start,
+// last NUL) as a small function: per entry mode, the exit mode, the record ends passed and
+// the last field boundary (a TAB read in K, a newline read in V); plus its last NUL.
+// These functions compose associatively (positions only grow, so "last" combines with
+// max), so each 16 KiB block gets its entry state from a device scan of block functions
+// and each thread from a block scan of the functions of its 128 bytes.
+//
+// The file is read ONCE (round 3; round 2 read it twice): pass A stages a block, finds
+// each span's events (NL / TAB / NUL) and packs up to six of them per span into one word,
+// computes the block function, and -- speculatively, since it does not know the mode at
+// the block's start -- hashes the key that would follow each of the block's newlines
+// (kSpec below).  Pass B needs no file bytes: from the packed events it rebuilds the span
+// functions, scans them, walks the events, writes every record and takes each key's hash
+// from pass A's state (or, for the rare key pass A could not cover, from the file).
 // ---------------------------------------------------------------------------
-constexpr int kTThreads = 128;
-constexpr int kTBytes = 128;                                    // bytes per thread
-constexpr uint64_t kTChunk = (uint64_t)kTThreads * kTBytes;     // 16 KiB per block
-constexpr int kTKeys = 256;                                     // LDS key list per block
+constexpr uint32_t kTThreads = 128;
+constexpr uint32_t kTBytes = 128;                               // bytes per thread
+constexpr uint32_t kTChunk = kTThreads * kTBytes;               // 16 KiB per block
 
 // Block-local function of a span; positions are block-relative + 1 (0: none).
 //   a: bit 0 / 1 = exit mode entering K / V (1 = V); bits [2, 17) / [17, 32) = record ends
@@ -424,53 +425,6 @@ __device__ inline uint32_t next_event(uint64_t& m0, uint64_t& m1) {
   return b;
 }
 
-// Pass A function of the thread's span at block-relative offset rel (positions + 1).
-__device__ inline LFn tsv_span_fn(const uint8_t* span, uint32_t rel) {
-  uint64_t mm[2];
-  tsv_events(span, mm[0], mm[1]);
-  uint32_t s0 = 0, s1 = 1, c0 = 0, c1 = 0, l0 = 0, l1 = 0, ln = 0;
-  // one loop over all events, the next event's byte read from LDS while this one is handled
-  uint32_t o = next_event(mm[0], mm[1]), c = span[o & 127u];
-  while (o < 128) {
-    const uint32_t on = next_event(mm[0], mm[1]), cn = span[on & 127u];
-    const uint32_t p1 = rel + o + 1;
-    if (c == 0x0Au) {
-      if (s0) ++c0, l0 = p1, s0 = 0;
-      if (s1) ++c1, l1 = p1, s1 = 0;
-    } else if (c == 0x09u) {
-      if (!s0) l0 = p1, s0 = 1;
-      if (!s1) l1 = p1, s1 = 1;
-    } else if (c == 0) {
-      ln = p1;
-    }
-    o = on;
-    c = cn;
-  }
-  return LFn{s0 | (s1 << 1) | (c0 << 2) | (c1 << 17), l0 | (l1 << 16), ln};
-}
-
-// Pass A: each block's function, and each thread's prefix within its block (three
-// coalesced words per thread, so pass B needs neither the span functions nor the scan).
-__global__ __launch_bounds__(kTThreads) void tsv_fn_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                           GFn* __restrict__ blk_fn, uint32_t* __restrict__ pa,
-                                                           uint32_t* __restrict__ pb, uint32_t* __restrict__ pc) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
-  typedef hipcub::BlockScan<LFn, kTThreads> Scan;
-  __shared__ typename Scan::TempStorage tmp;
-  tsv_stage(f, size, blockIdx.x, lds);
-  const uint32_t rel = kTBytes * threadIdx.x;
-  const LFn t = (uint64_t)blockIdx.x * kTChunk + rel < size ? tsv_span_fn(lds + 16 + rel, rel) : lfn_id();
-  LFn pre, agg;
-  Scan(tmp).ExclusiveScan(t, pre, lfn_id(), LCompose(), agg);
-  const uint64_t i = (uint64_t)blockIdx.x * kTThreads + threadIdx.x;
-  if (pa) {
-    pa[i] = pre.a;
-    pb[i] = pre.b;
-    pc[i] = pre.c;
-  }
-  if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(agg, (uint64_t)blockIdx.x * kTChunk);
-}
-
 // Record count: the whole file's function from the start state, plus the record a
 // value getline ends at EOF.
 __global__ void tsv_count_kernel(const GFn* __restrict__ excl, const GFn* __restrict__ blk_fn, uint64_t nblk,
@@ -479,74 +433,261 @@ __global__ void tsv_count_kernel(const GFn* __restrict__ excl, const GFn* __rest
   out[0] = e.r + e.m;
 }
 
-// Key hash from the staged block (key [off, off + len) inside it; chunk 0 may read up to
-// 15 bytes below, into the pad or the block's own earlier bytes, masked): h1 / h2 of the
-// key + NUL as hash_cstr computes them.
-__device__ inline void hash_cstr_lds(const uint8_t* lds_key, uint64_t len, const SpadTable& sp, uint64_t& h1,
-                                     uint64_t& h2) {
-  uint64_t raw = sp.v[0];
-  if (len) {
-    const uint32_t k = (uint32_t)((len + 15) / 16), p = (uint32_t)(16 * k - len);
-    const uint8_t* c0 = lds_key - p;
-    uint4 c = ld16(c0);
-    const uint32_t m0 = p >= 4 ? 0u : ~0u << (8 * p), m1 = p >= 8 ? 0u : p <= 4 ? ~0u : ~0u << (8 * (p - 4));
-    const uint32_t m2 = p >= 12 ? 0u : p <= 8 ? ~0u : ~0u << (8 * (p - 8)), m3 = p <= 12 ? ~0u : ~0u << (8 * (p - 12));
-    c.x &= m0, c.y &= m1, c.z &= m2, c.w &= m3;
-    uint32_t lo = (uint32_t)sp.v[p], hi = (uint32_t)(sp.v[p] >> 32);
-    for (uint32_t q = 1; q < k; ++q) {
-      const uint4 nx = ld16(c0 + 16 * q);
-      fnv_chunk16(lo, hi, c);
-      c = nx;
+// Events of a thread's span: NL / TAB / NUL bytes (types 1 / 2 / 3) in byte order.  Pass A
+// packs up to kEvCap of them into one word per thread for pass B: entry j = offset (7 bits)
+// | type << 7 at bits [9j, 9j + 9), the count at bits [56, 60); count 15 = more than kEvCap
+// (pass B re-reads that span from the file).
+constexpr uint32_t kEvCap = 6;
+constexpr uint64_t kEvOverflow = 15ull << 56;
+__device__ inline uint32_t ev_type(uint32_t c) { return c == 0x0Au ? 1u : c == 0x09u ? 2u : c == 0u ? 3u : 0u; }
+
+// The span function (positions + 1) of an event sequence: per entry mode the exit mode, the
+// record ends passed and the last boundary; the last NUL.
+struct FnAcc {
+  uint32_t s0 = 0, s1 = 1, c0 = 0, c1 = 0, l0 = 0, l1 = 0, ln = 0;
+  __device__ void add(uint32_t type, uint32_t p1) {
+    if (type == 1u) {
+      if (s0) ++c0, l0 = p1, s0 = 0;
+      if (s1) ++c1, l1 = p1, s1 = 0;
+    } else if (type == 2u) {
+      if (!s0) l0 = p1, s0 = 1;
+      if (!s1) l1 = p1, s1 = 1;
+    } else if (type == 3u) {
+      ln = p1;
     }
-    fnv_chunk16(lo, hi, c);
-    raw = ((uint64_t)hi << 32) | lo;
   }
-  h1 = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
-  h2 = len ? raw : h1;
+  __device__ LFn fn() const { return LFn{s0 | (s1 << 1) | (c0 << 2) | (c1 << 17), l0 | (l1 << 16), ln}; }
+};
+
+// Walk the events of a span staged at `span` (its candidate masks), calling f(offset, type).
+template <class F>
+__device__ inline void span_events(const uint8_t* span, F&& f) {
+  uint64_t mm[2];
+  tsv_events(span, mm[0], mm[1]);
+  uint32_t o = next_event(mm[0], mm[1]), c = span[o & 127u];
+  while (o < 128) {
+    const uint32_t on = next_event(mm[0], mm[1]), cn = span[on & 127u];
+    const uint32_t t = ev_type(c);
+    if (t) f(o, t);
+    o = on;
+    c = cn;
+  }
 }
 
-// Pass B: the walk.  Fields are written (and keys hashed) only for records below
-// min(count, cap), so a key cut off by EOF writes nothing.
-template <bool HASH>
-__global__ __launch_bounds__(kTThreads) void tsv_walk_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                             const GFn* __restrict__ excl,
-                                                             const uint32_t* __restrict__ pa,
-                                                             const uint32_t* __restrict__ pb,
-                                                             const uint32_t* __restrict__ pc,
-                                                             const uint64_t* __restrict__ count, uint64_t cap,
-                                                             k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
-                                                             uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+// Key of the C string a record stores, from LDS: raw FNV state of the key's bytes (the
+// second hash of key + NUL; the first is raw * P), seed for the empty key.
+__device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, const SpadTable& sp) {
+  if (!len) return sp.v[0];
+  const uint32_t k = (len + 15) / 16, p = 16 * k - len;
+  const uint8_t* c0 = lds_key - p;
+  uint4 c = ld16(c0);
+  const uint32_t m0 = p >= 4 ? 0u : ~0u << (8 * p), m1 = p >= 8 ? 0u : p <= 4 ? ~0u : ~0u << (8 * (p - 4));
+  const uint32_t m2 = p >= 12 ? 0u : p <= 8 ? ~0u : ~0u << (8 * (p - 8)), m3 = p <= 12 ? ~0u : ~0u << (8 * (p - 12));
+  c.x &= m0, c.y &= m1, c.z &= m2, c.w &= m3;
+  uint32_t lo = (uint32_t)sp.v[p], hi = (uint32_t)(sp.v[p] >> 32);
+  for (uint32_t q = 1; q < k; ++q) {
+    const uint4 nx = ld16(c0 + 16 * q);
+    fnv_chunk16(lo, hi, c);
+    c = nx;
+  }
+  fnv_chunk16(lo, hi, c);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Speculative keys: pass A does not know the mode at its block's start, but a key starts
+// exactly after every newline the value getline reads -- so for the k-th newline of the
+// block (k < kSpec) it hashes the bytes from the newline + 1 to the first TAB or NUL after
+// it (the key getline's TAB, the C-string cut), when that cut lies inside the block.  Pass
+// B uses the stored state for every key that starts after a newline of its block; every
+// other key (the file's first, a key whose newline is in an earlier block, a cut beyond
+// the block, a span with more than kEvCap events) is hashed from the file.
+constexpr uint32_t kSpec = 256;
+
+// Pass A: each block's function (for the block scan), each thread's packed events, and the
+// speculative key states with their validity bits.
+__global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                          GFn* __restrict__ blk_fn, uint64_t* __restrict__ ev,
+                                                          uint64_t* __restrict__ spec, uint32_t* __restrict__ spec_ok,
+                                                          SpadTable sp) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
-  __shared__ uint64_t kl_off[HASH ? kTKeys : 1], kl_rec[HASH ? kTKeys : 1];
-  __shared__ uint32_t kl_len[HASH ? kTKeys : 1], kl_n;
-  if (HASH && threadIdx.x == 0) kl_n = 0;
-  tsv_stage(f, size, blockIdx.x, lds);  // (its barrier also publishes kl_n = 0)
-  const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
+  __shared__ uint64_t s_m[2 * kTThreads];  // candidate masks of every span
+  __shared__ uint32_t s_klen[kSpec], s_kstart[kSpec], s_ok[kSpec / 32], s_nk;
+  typedef hipcub::BlockScan<LFn, kTThreads> Scan;
+  typedef hipcub::BlockScan<uint32_t, kTThreads> CScan;
+  __shared__ typename Scan::TempStorage tmp;
+  __shared__ typename CScan::TempStorage ctmp;
+  if (threadIdx.x < kSpec / 32) s_ok[threadIdx.x] = 0;
+  if (threadIdx.x == 0) s_nk = 0;
+  tsv_stage(f, size, blockIdx.x, lds);
   const uint32_t rel = kTBytes * threadIdx.x;
   const uint8_t* span = lds + 16 + rel;
+  const bool live = (uint64_t)blockIdx.x * kTChunk + rel < size;
+  uint64_t m0 = 0, m1 = 0;
+  if (live) tsv_events(span, m0, m1);
+  s_m[2 * threadIdx.x] = m0;
+  s_m[2 * threadIdx.x + 1] = m1;
+  FnAcc acc;
+  uint64_t pk = 0;
+  uint32_t ne = 0, nnl = 0;
+  if (live)
+    span_events(span, [&](uint32_t o, uint32_t t) {
+      acc.add(t, rel + o + 1);
+      if (ne < kEvCap) pk |= (uint64_t)(o | (t << 7)) << (9 * ne);
+      ++ne;
+      nnl += t == 1u;
+    });
+  ev[(uint64_t)blockIdx.x * kTThreads + threadIdx.x] = ne > kEvCap ? kEvOverflow : pk | ((uint64_t)ne << 56);
+  LFn pre, agg;
+  Scan(tmp).ExclusiveScan(live ? acc.fn() : lfn_id(), pre, lfn_id(), LCompose(), agg);
+  uint32_t k0;
+  CScan(ctmp).ExclusiveSum(nnl, k0);
+  if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(agg, (uint64_t)blockIdx.x * kTChunk);
+  __syncthreads();  // s_m of every span
+  // this span's newlines: the key after each, cut at the first TAB / NUL after it
+  if (live && k0 < kSpec) {
+    uint32_t k = k0;
+    span_events(span, [&](uint32_t o, uint32_t t) {
+      if (t != 1u || k >= kSpec) return;
+      const uint32_t start = rel + o + 1;  // block-relative
+      uint32_t cut = kTChunk;              // none in the block
+      uint32_t th = start / kTBytes, bit = start % kTBytes;
+      while (th < kTThreads && cut == kTChunk) {
+        uint64_t a = s_m[2 * th], b = s_m[2 * th + 1];
+        if (bit >= 64) a = 0, b &= bit >= 128 ? 0 : ~0ull << (bit - 64);
+        else a &= ~0ull << bit;
+        while (a | b) {
+          const uint32_t q = a ? (uint32_t)__builtin_ctzll(a) : 64u + (uint32_t)__builtin_ctzll(b);
+          if (a) a &= a - 1;
+          else b &= b - 1;
+          const uint32_t c = lds[16 + th * kTBytes + q];
+          if (c == 0x09u || c == 0u) {
+            cut = th * kTBytes + q;
+            break;
+          }
+        }
+        ++th;
+        bit = 0;
+      }
+      if (cut < kTChunk && (uint64_t)blockIdx.x * kTChunk + cut < size) {
+        const uint32_t slot = atomicAdd(&s_nk, 1u);
+        s_kstart[slot] = start | (k << 16);
+        s_klen[slot] = cut - start;
+      }
+      ++k;
+    });
+  }
+  __syncthreads();
+  const uint32_t nk = s_nk;
+  for (uint32_t i = threadIdx.x; i < nk; i += kTThreads) {
+    const uint32_t start = s_kstart[i] & 0xFFFFu, k = s_kstart[i] >> 16;
+    spec[(uint64_t)blockIdx.x * kSpec + k] = key_raw_lds(lds + 16 + start, s_klen[i], sp);
+    atomicOr(&s_ok[k / 32], 1u << (k % 32));
+  }
+  __syncthreads();
+  if (threadIdx.x < kSpec / 32) spec_ok[(uint64_t)blockIdx.x * (kSpec / 32) + threadIdx.x] = s_ok[threadIdx.x];
+}
+
+// Pass B: each thread's events (packed by pass A, or re-read from the file for a span with
+// more than kEvCap), the block scan of the span functions again (from the events: no
+// prefixes stored), the walk, the records, and every key's h1 / h2 -- the speculative
+// state when pass A computed it, else hashed from the file.  Fields are written only for
+// records below min(count, cap), so a key cut off by EOF writes nothing.
+template <bool HASH>
+__global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restrict__ f, uint64_t size,
+                                                          const GFn* __restrict__ excl, const uint64_t* __restrict__ ev,
+                                                          const uint64_t* __restrict__ spec,
+                                                          const uint32_t* __restrict__ spec_ok,
+                                                          const uint64_t* __restrict__ count, uint64_t cap,
+                                                          k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
+                                                          uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+  __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];  // overflowing spans only
+  __shared__ uint64_t s_ev[kTThreads];
+  __shared__ uint32_t s_nl[kTThreads], s_ok[kSpec / 32];
+  typedef hipcub::BlockScan<LFn, kTThreads> Scan;
+  typedef hipcub::BlockScan<uint32_t, kTThreads> CScan;
+  __shared__ typename Scan::TempStorage tmp;
+  __shared__ typename CScan::TempStorage ctmp;
+  const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
+  const uint32_t rel = kTBytes * threadIdx.x;
   const bool live = base + rel < size;
-  const uint64_t ti = (uint64_t)blockIdx.x * kTThreads + threadIdx.x;
-  const LFn pre{pa[ti], pb[ti], pc[ti]};
+  const uint64_t pk = ev[(uint64_t)blockIdx.x * kTThreads + threadIdx.x];
+  const bool over = pk == kEvOverflow;
+  if (HASH && threadIdx.x < kSpec / 32) s_ok[threadIdx.x] = spec_ok[(uint64_t)blockIdx.x * (kSpec / 32) + threadIdx.x];
+  uint8_t* span = lds + 16 + rel;
+  if (over) {  // rare: stage this span's 128 bytes (bytes past the file read as 0x01)
+    for (uint32_t q = 0; q < kTBytes; q += 4) {
+      uint32_t x = 0x01010101u;
+      for (uint32_t j = 0; j < 4; ++j)
+        if (base + rel + q + j < size) x = (x & ~(0xFFu << (8 * j))) | ((uint32_t)f[base + rel + q + j] << (8 * j));
+      *reinterpret_cast<uint32_t*>(span + q) = x;
+    }
+  }
+  auto for_events = [&](auto&& fn) {
+    if (!live) return;
+    if (over) {
+      span_events(span, fn);
+    } else {
+      const uint32_t ne = (uint32_t)(pk >> 56) & 15u;
+      for (uint32_t j = 0; j < ne; ++j) {
+        const uint32_t e = (uint32_t)(pk >> (9 * j)) & 0x1FFu;
+        fn(e & 127u, e >> 7);
+      }
+    }
+  };
+  FnAcc acc;
+  uint32_t nnl = 0;
+  for_events([&](uint32_t o, uint32_t t) {
+    acc.add(t, rel + o + 1);
+    nnl += t == 1u;
+  });
+  LFn pre;
+  Scan(tmp).ExclusiveScan(live ? acc.fn() : lfn_id(), pre, lfn_id(), LCompose());
+  uint32_t k0;
+  CScan(ctmp).ExclusiveSum(nnl, k0);
+  s_ev[threadIdx.x] = over ? kEvOverflow : pk;
+  s_nl[threadIdx.x] = k0;
+  __syncthreads();
   TState s = gapply(gfn_of(pre, base), gapply(excl[blockIdx.x], TState{0, 0, 0, 0}));
   const uint64_t lim = min(count[0], cap);
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
+  // the newline index within the block of the newline at block-relative position q, or
+  // kSpec when unknown (its span overflowed)
+  auto nl_index = [&](uint32_t q) -> uint32_t {
+    const uint32_t th = q / kTBytes, o = q % kTBytes;
+    const uint64_t w = s_ev[th];
+    if (w == kEvOverflow) return kSpec;
+    const uint32_t ne = (uint32_t)(w >> 56) & 15u;
+    uint32_t k = s_nl[th];
+    for (uint32_t j = 0; j < ne; ++j) {
+      const uint32_t e = (uint32_t)(w >> (9 * j)) & 0x1FFu;
+      if ((e & 127u) >= o) break;
+      k += (e >> 7) == 1u;
+    }
+    return k;
+  };
   auto key_end = [&](uint64_t e) {
     if (s.r >= lim) return;
     recs[s.r].key_off = s.fs;
     recs[s.r].key_len = e - s.fs;
     if constexpr (HASH) {
-      uint32_t slot = kTKeys;
-      if (s.fs >= base) slot = __hip_atomic_fetch_add(&kl_n, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      if (slot < kTKeys) {
-        kl_off[slot] = s.fs;
-        kl_len[slot] = (uint32_t)(e - s.fs);
-        kl_rec[slot] = s.r;
-      } else {  // starts before the block, or the list is full: hash it here from HBM
-        uint64_t a, c;
-        hash_cstr(f, s.fs, e - s.fs, sp, a, c);
-        h1[s.r] = a;
-        if (h2) h2[s.r] = c;
+      uint64_t raw = 0;
+      bool got = false;
+      if (s.fs > base && s.fs - 1 < base + kTChunk) {
+        const uint32_t k = nl_index((uint32_t)(s.fs - 1 - base));
+        if (k < kSpec && ((s_ok[k / 32] >> (k % 32)) & 1u)) {
+          raw = spec[(uint64_t)blockIdx.x * kSpec + k];
+          got = true;
+        }
       }
+      uint64_t a, c;
+      if (got) {
+        a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
+        c = e > s.fs ? raw : a;
+      } else {
+        hash_cstr(f, s.fs, e - s.fs, sp, a, c);
+      }
+      h1[s.r] = a;
+      if (h2) h2[s.r] = c;
     }
   };
   auto val_end = [&](uint64_t e) {
@@ -554,51 +695,31 @@ __global__ __launch_bounds__(kTThreads) void tsv_walk_kernel(const uint8_t* __re
     recs[s.r].val_off = s.fs;
     recs[s.r].val_len = e - s.fs;
   };
-  if (live) {
-    uint64_t mm[2];
-    tsv_events(span, mm[0], mm[1]);
-    uint32_t o = next_event(mm[0], mm[1]), c = span[o & 127u];
-    while (o < 128) {
-      const uint32_t on = next_event(mm[0], mm[1]), cn = span[on & 127u];
-      {
-        const uint64_t pos = base + rel + o;
-        if (c == 0x0Au) {
-          if (s.m) {  // the value getline's newline: the record ends
-            if (!nulf) val_end(pos);
-            s.m = 0;
-            ++s.r;
-            s.fs = pos + 1;
-            nulf = false;
-          }
-        } else if (c == 0x09u) {
-          if (!s.m) {  // the key getline's TAB
-            if (!nulf) key_end(pos);
-            s.m = 1;
-            s.fs = pos + 1;
-            nulf = false;
-          }
-        } else if (c == 0 && !nulf) {  // the field's first NUL: its C string ends here
-          if (s.m) val_end(pos);
-          else key_end(pos);
-          nulf = true;
-        }
+  for_events([&](uint32_t o, uint32_t t) {
+    const uint64_t pos = base + rel + o;
+    if (t == 1u) {
+      if (s.m) {  // the value getline's newline: the record ends
+        if (!nulf) val_end(pos);
+        s.m = 0;
+        ++s.r;
+        s.fs = pos + 1;
+        nulf = false;
       }
-      o = on;
-      c = cn;
+    } else if (t == 2u) {
+      if (!s.m) {  // the key getline's TAB
+        if (!nulf) key_end(pos);
+        s.m = 1;
+        s.fs = pos + 1;
+        nulf = false;
+      }
+    } else if (!nulf) {  // the field's first NUL: its C string ends here
+      if (s.m) val_end(pos);
+      else key_end(pos);
+      nulf = true;
     }
-    // the thread holding the last byte: a value read to EOF
-    if (base + rel + kTBytes >= size && s.m && !nulf) val_end(size);
-  }
-  if constexpr (HASH) {
-    __syncthreads();
-    const uint32_t nk = min(kl_n, (uint32_t)kTKeys);
-    for (uint32_t i = threadIdx.x; i < nk; i += kTThreads) {
-      uint64_t a, c;
-      hash_cstr_lds(lds + 16 + (kl_off[i] - base), kl_len[i], sp, a, c);
-      h1[kl_rec[i]] = a;
-      if (h2) h2[kl_rec[i]] = c;
-    }
-  }
+  });
+  // the thread holding the last byte: a value read to EOF
+  if (live && base + rel + kTBytes >= size && s.m && !nulf) val_end(size);
 }
 
 }  // namespace
@@ -640,58 +761,31 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
   return pools[dev] ? hipMallocFromPoolAsync(p, bytes, pools[dev], stream) : hipMallocAsync(p, bytes, stream);
 }
 
-// The TSV per-thread prefixes (12 B per 128 B of file): a grow-only buffer per device,
-// held across calls while it stays within kScratchKeep (larger ones are freed at the end
-// of the call), under a per-device lock for the duration of the call -- a pool
-// allocation of this size cost ~0.5 ms per call.
-struct PrefixCache {
-  std::mutex mu;
-  void* p = nullptr;
-  size_t bytes = 0;
-};
-PrefixCache g_prefix[64];
-
 // TSV: pass A, the scan of block functions, the count, pass B (when recs), one read-back.
+// Temporaries per 16 KiB block: its function (2 x 48 B), 8 B of events per 128 B span,
+// and kSpec speculative key states + their validity bits (~2 KiB, mostly unwritten).
 static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
                       hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
   const uint64_t nblk = (size + kTChunk - 1) / kTChunk;
   GFn *fn = nullptr, *excl = nullptr;
-  uint64_t* dcount = nullptr;
-  uint32_t* pre = nullptr;
+  uint64_t *dcount = nullptr, *ev = nullptr, *spec = nullptr;
+  uint32_t* spec_ok = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   hipError_t e = nblk > 0x7FFFFFFFull ? hipErrorInvalidValue : hipSuccess;
   auto tr = [&](hipError_t x) {
     if (e == hipSuccess) e = x;
   };
+  const bool walk = recs && cap;
   tr(scratch_alloc((void**)&fn, nblk * sizeof(GFn), stream));
   tr(scratch_alloc((void**)&excl, nblk * sizeof(GFn), stream));
   tr(scratch_alloc((void**)&dcount, 8, stream));
-  const bool walk = recs && cap;
-  int dev = 0;
-  tr(hipGetDevice(&dev));
-  if (e == hipSuccess && (dev < 0 || dev >= 64)) e = hipErrorInvalidDevice;
-  PrefixCache& pc_ = g_prefix[e == hipSuccess ? dev : 0];
-  std::unique_lock<std::mutex> lk(pc_.mu, std::defer_lock);
-  const size_t pre_bytes = walk ? nblk * kTThreads * 12 : 0;
-  if (e == hipSuccess && walk) {
-    lk.lock();
-    if (pc_.bytes < pre_bytes) {
-      if (pc_.p) tr(hipFree(pc_.p));
-      pc_.p = nullptr;
-      pc_.bytes = 0;
-      tr(hipMalloc(&pc_.p, pre_bytes));
-      if (e == hipSuccess) pc_.bytes = pre_bytes;
-    }
-    pre = (uint32_t*)pc_.p;
-  }
-  uint32_t *pa = pre, *pb = pre + (walk ? nblk * kTThreads : 0), *pc = pb + (walk ? nblk * kTThreads : 0);
+  tr(scratch_alloc((void**)&ev, nblk * kTThreads * 8, stream));
+  tr(scratch_alloc((void**)&spec, nblk * kSpec * 8, stream));
+  tr(scratch_alloc((void**)&spec_ok, nblk * (kSpec / 32) * 4, stream));
+  const SpadTable sp = make_spad(seed);
   if (e == hipSuccess) {
-    // (count only: no prefixes)
-    if (walk)
-      tsv_fn_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, pa, pb, pc);
-    else
-      tsv_fn_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, nullptr, nullptr, nullptr);
+    tsv_a_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, ev, spec, spec_ok, sp);
     e = hipGetLastError();
   }
   tr(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp_bytes, fn, excl, GCompose(), gfn_id(), nblk, stream));
@@ -701,25 +795,20 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
     tsv_count_kernel<<<1, 1, 0, stream>>>(excl, fn, nblk, dcount);
     e = hipGetLastError();
   }
-  if (e == hipSuccess && recs && cap) {
+  if (e == hipSuccess && walk) {
     if (h1)
-      tsv_walk_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, pa, pb, pc, dcount, cap, recs,
-                                                                      make_spad(seed), h1, h2);
+      tsv_b_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, ev, spec, spec_ok, dcount, cap, recs,
+                                                                   sp, h1, h2);
     else
-      tsv_walk_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, pa, pb, pc, dcount, cap, recs,
-                                                                       SpadTable{}, nullptr, nullptr);
+      tsv_b_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, ev, spec, spec_ok, dcount, cap,
+                                                                    recs, sp, nullptr, nullptr);
     e = hipGetLastError();
   }
   uint64_t n = 0;
   tr(hipMemcpyAsync(&n, dcount, 8, hipMemcpyDeviceToHost, stream));
   tr(hipStreamSynchronize(stream));
-  for (void* p : {(void*)fn, (void*)excl, (void*)dcount, tmp})
+  for (void* p : {(void*)fn, (void*)excl, (void*)dcount, (void*)ev, (void*)spec, (void*)spec_ok, tmp})
     if (p) (void)hipFreeAsync(p, stream);
-  if (lk.owns_lock() && pc_.bytes > kScratchKeep) {  // the stream is synchronised: no kernel still reads it
-    (void)hipFree(pc_.p);
-    pc_.p = nullptr;
-    pc_.bytes = 0;
-  }
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;
   *count = n;

@@ -9,6 +9,6 @@ rm -rf $O; mkdir -p $O
 i=0
 for c in "FETCH_SIZE" "WRITE_SIZE" "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_BUSY_CYCLES"; do
   i=$((i+1))
-  (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex "tsv_|rocprim|fill" --output-format csv -d $O/pmc$i -o pmc -- python3 $R/tools/import_step.py --calls 4 > $O/pmc$i.log 2>&1)
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $c --kernel-include-regex "tsv_|rocprim" --output-format csv -d $O/pmc$i -o pmc -- python3 $R/tools/import_step.py --calls 4 > $O/pmc$i.log 2>&1)
 done
 echo IMPORT_PROFILE_OK

@@ -1,6 +1,6 @@
 """Summarise tools/gpu/r02ar.sh (rocprofv3 over tools/import_step.py): per call of
 k2h_amd_import_scan_prehash_device, the kernel time and the PMC counters summed over its
-kernels (tsv_fn, the block-function scan, tsv_count, tsv_walk), averaged over the last
+kernels (tsv_a, the block-function scan, tsv_count, tsv_b), averaged over the last
 calls -> profiles/traffic_import.json, profiles/valu_import.json (bench.py's
 secondary.import roofline) and profiles/<tag>_import_summary.json.
 
@@ -15,7 +15,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-OURS = ("tsv_fn_kernel", "tsv_count_kernel", "tsv_walk_kernel", "ROCPRIM_400200")  # rocprim 4.2: our scan
+OURS = ("tsv_a_kernel", "tsv_count_kernel", "tsv_b_kernel", "ROCPRIM_400200")  # rocprim 4.2: our scan
 
 
 def ours(name):
@@ -27,7 +27,7 @@ def main():
     prof = ROOT / "profiles"
     # kernel time per call from the trace: the last 10 calls' dispatches of our kernels
     rows = [r for r in csv.DictReader(open(src / "trace" / "run_kernel_trace.csv")) if ours(r["Kernel_Name"])]
-    walks = [i for i, r in enumerate(rows) if "tsv_walk_kernel" in r["Kernel_Name"]]
+    walks = [i for i, r in enumerate(rows) if "tsv_b_kernel" in r["Kernel_Name"]]
     calls = 10
     first = walks[-calls - 1] + 1
     per = collections.defaultdict(float)
@@ -44,21 +44,21 @@ def main():
         if not fs:
             continue
         crow = [r for r in csv.DictReader(open(fs[0])) if ours(r["Kernel_Name"])]
-        ncalls = len({r["Dispatch_Id"] for r in crow if "tsv_walk_kernel" in r["Kernel_Name"]})
+        ncalls = len({r["Dispatch_Id"] for r in crow if "tsv_b_kernel" in r["Kernel_Name"]})
         acc = collections.defaultdict(float)
         for r in crow:
             acc[r["Counter_Name"]] += float(r["Counter_Value"])
         for k, v in acc.items():
             pmc[k] = v / ncalls
     traffic = int(2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024)
-    kern = "tsv_fn_kernel + block-function scan + tsv_count_kernel + tsv_walk_kernel<true> (one call)"
+    kern = "tsv_a_kernel + block-function scan + tsv_count_kernel + tsv_b_kernel<true> (one call)"
     (prof / "traffic_import.json").write_text(json.dumps({
         "kernel": kern, "hbm_bytes_per_launch": traffic, "FETCH_SIZE_kB": pmc["FETCH_SIZE"],
         "WRITE_SIZE_kB": pmc["WRITE_SIZE"], "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
-        "round": tag}, indent=1) + "\n")
+        "round": tag, "keys_per_launch": 1 << 23}, indent=1) + "\n")
     (prof / "valu_import.json").write_text(json.dumps({
         "kernel": kern, "valu_insts_per_launch": pmc["SQ_INSTS_VALU"], "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"),
-        "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"), "round": tag}, indent=1) + "\n")
+        "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"), "round": tag, "keys_per_launch": 1 << 23}, indent=1) + "\n")
     s = {"per_kernel_us_per_call": {k: v / 1e3 for k, v in per.items()}, "gpu_us_per_call": gpu_us,
          "pmc_per_call": pmc, "hbm_bytes_per_call": traffic,
          "source": "tools/gpu/r02ar.sh: rocprofv3 over tools/import_step.py (8M-record TSV, 1.16 GB)"}
