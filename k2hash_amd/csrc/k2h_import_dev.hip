@@ -495,124 +495,132 @@ __device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, con
 }
 
 // Speculative keys: pass A does not know the mode at its block's start, but a key starts
-// exactly after every newline the value getline reads -- so for the k-th newline of the
-// block (k < kSpec) it hashes the bytes from the newline + 1 to the first TAB or NUL after
-// it (the key getline's TAB, the C-string cut), when that cut lies inside the block.  Pass
-// B uses the stored state for every key that starts after a newline of its block; every
-// other key (the file's first, a key whose newline is in an earlier block, a cut beyond
-// the block, a span with more than kEvCap events) is hashed from the file.
-constexpr uint32_t kSpec = 256;
+// exactly after every newline the value getline reads, and ends at the first TAB or NUL
+// after it (the key getline's TAB, or the C-string cut).  So for every cut event (TAB /
+// NUL) that is the first after a newline of the same block, pass A hashes the bytes
+// between them and stores the raw state with the key's start in the cut's slot: slot j of
+// span t = the j-th cut event of that span (j < kSlots; pk bit 60 + j marks it written).
+// Pass B, whose walk ends a key at cut event j of its span, takes the slot when the key's
+// true start equals the stored one; every other key (the file's first, a key whose newline
+// is in an earlier block, a third cut in one span, a span with more than kEvCap events)
+// is hashed from the file.
+constexpr uint32_t kSlots = 2;
+struct alignas(16) SpecSlot {
+  uint64_t raw;    // FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
+  uint32_t start;  // block-relative start of the key
+  uint32_t pad;
+};
 
-// Pass A: each block's function (for the block scan), each thread's packed events, and the
-// speculative key states with their validity bits.
+// Newline state of a span for the speculative keys: whether it holds a newline, whether
+// the last one is still open (no cut after it), and its block-relative position; composed
+// in file order (a later newline resets, a cut closes).
+struct NlSum {
+  uint32_t v;  // bit 0: has newline, bit 1: open, bits [2, 18): last newline position
+};
+__device__ inline NlSum nl_compose(NlSum x, NlSum y) {
+  if (y.v & 1u) return y;
+  return NlSum{x.v & ((y.v & 2u) ? ~0u : ~2u)};  // y has no newline; its bit 1 = "no cut in y"
+}
+struct ScanA {
+  LFn fn;
+  NlSum nl;
+};
+struct ScanAOp {
+  __device__ ScanA operator()(const ScanA& x, const ScanA& y) const { return ScanA{LCompose()(x.fn, y.fn), nl_compose(x.nl, y.nl)}; }
+};
+
+// Pass A: each block's function (for the device scan), each thread's packed events, and
+// the speculative key states.
 __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                           GFn* __restrict__ blk_fn, uint64_t* __restrict__ ev,
-                                                          uint64_t* __restrict__ spec, uint32_t* __restrict__ spec_ok,
-                                                          SpadTable sp) {
+                                                          SpecSlot* __restrict__ spec, SpadTable sp) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
-  __shared__ uint64_t s_m[2 * kTThreads];  // candidate masks of every span
-  __shared__ uint32_t s_klen[kSpec], s_kstart[kSpec], s_ok[kSpec / 32], s_nk;
-  typedef hipcub::BlockScan<LFn, kTThreads> Scan;
-  typedef hipcub::BlockScan<uint32_t, kTThreads> CScan;
+  typedef hipcub::BlockScan<ScanA, kTThreads> Scan;
   __shared__ typename Scan::TempStorage tmp;
-  __shared__ typename CScan::TempStorage ctmp;
-  if (threadIdx.x < kSpec / 32) s_ok[threadIdx.x] = 0;
-  if (threadIdx.x == 0) s_nk = 0;
   tsv_stage(f, size, blockIdx.x, lds);
   const uint32_t rel = kTBytes * threadIdx.x;
   const uint8_t* span = lds + 16 + rel;
-  const bool live = (uint64_t)blockIdx.x * kTChunk + rel < size;
-  uint64_t m0 = 0, m1 = 0;
-  if (live) tsv_events(span, m0, m1);
-  s_m[2 * threadIdx.x] = m0;
-  s_m[2 * threadIdx.x + 1] = m1;
+  const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
+  const bool live = base + rel < size;
   FnAcc acc;
   uint64_t pk = 0;
-  uint32_t ne = 0, nnl = 0;
+  uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
   if (live)
     span_events(span, [&](uint32_t o, uint32_t t) {
       acc.add(t, rel + o + 1);
       if (ne < kEvCap) pk |= (uint64_t)(o | (t << 7)) << (9 * ne);
       ++ne;
-      nnl += t == 1u;
+      if (t == 1u) nl = 1u | 2u | ((rel + o) << 2);
+      else nl &= ~2u;
     });
-  ev[(uint64_t)blockIdx.x * kTThreads + threadIdx.x] = ne > kEvCap ? kEvOverflow : pk | ((uint64_t)ne << 56);
-  LFn pre, agg;
-  Scan(tmp).ExclusiveScan(live ? acc.fn() : lfn_id(), pre, lfn_id(), LCompose(), agg);
-  uint32_t k0;
-  CScan(ctmp).ExclusiveSum(nnl, k0);
-  if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(agg, (uint64_t)blockIdx.x * kTChunk);
-  __syncthreads();  // s_m of every span
-  // this span's newlines: the key after each, cut at the first TAB / NUL after it
-  if (live && k0 < kSpec) {
-    uint32_t k = k0;
-    span_events(span, [&](uint32_t o, uint32_t t) {
-      if (t != 1u || k >= kSpec) return;
-      const uint32_t start = rel + o + 1;  // block-relative
-      uint32_t cut = kTChunk;              // none in the block
-      uint32_t th = start / kTBytes, bit = start % kTBytes;
-      while (th < kTThreads && cut == kTChunk) {
-        uint64_t a = s_m[2 * th], b = s_m[2 * th + 1];
-        if (bit >= 64) a = 0, b &= bit >= 128 ? 0 : ~0ull << (bit - 64);
-        else a &= ~0ull << bit;
-        while (a | b) {
-          const uint32_t q = a ? (uint32_t)__builtin_ctzll(a) : 64u + (uint32_t)__builtin_ctzll(b);
-          if (a) a &= a - 1;
-          else b &= b - 1;
-          const uint32_t c = lds[16 + th * kTBytes + q];
-          if (c == 0x09u || c == 0u) {
-            cut = th * kTBytes + q;
-            break;
-          }
-        }
-        ++th;
-        bit = 0;
+  const bool over = ne > kEvCap;
+  pk = over ? kEvOverflow : pk | ((uint64_t)ne << 56);
+  ScanA pre, agg;
+  Scan(tmp).ExclusiveScan(ScanA{live ? acc.fn() : lfn_id(), NlSum{live ? nl : 2u}}, pre,
+                          ScanA{lfn_id(), NlSum{2u}}, ScanAOp(), agg);
+  if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(agg.fn, base);
+  // keys ending at this span's cuts: the newline state entering the span, then its events
+  bool open = (pre.nl.v & 3u) == 3u;
+  uint32_t start = (pre.nl.v >> 2) + 1, j = 0;
+  auto emit = [&](uint32_t o, uint32_t t) {
+    const uint32_t pos = rel + o;
+    if (t == 1u) {
+      open = true;
+      start = pos + 1;
+      return;
+    }
+    if (open && j < kSlots && base + pos < size) {  // the first cut after a newline of this block
+      SpecSlot s;
+      s.raw = key_raw_lds(lds + 16 + start, pos - start, sp);
+      s.start = start;
+      s.pad = 0;
+      spec[((uint64_t)blockIdx.x * kTThreads + threadIdx.x) * kSlots + j] = s;
+      if (!over) pk |= 1ull << (60 + j);
+    }
+    open = false;
+    ++j;
+  };
+  if (live) {
+    if (over) {
+      span_events(span, emit);
+    } else {
+      for (uint32_t q = 0; q < ne; ++q) {
+        const uint32_t e = (uint32_t)(pk >> (9 * q)) & 0x1FFu;
+        emit(e & 127u, e >> 7);
       }
-      if (cut < kTChunk && (uint64_t)blockIdx.x * kTChunk + cut < size) {
-        const uint32_t slot = atomicAdd(&s_nk, 1u);
-        s_kstart[slot] = start | (k << 16);
-        s_klen[slot] = cut - start;
-      }
-      ++k;
-    });
+    }
   }
-  __syncthreads();
-  const uint32_t nk = s_nk;
-  for (uint32_t i = threadIdx.x; i < nk; i += kTThreads) {
-    const uint32_t start = s_kstart[i] & 0xFFFFu, k = s_kstart[i] >> 16;
-    spec[(uint64_t)blockIdx.x * kSpec + k] = key_raw_lds(lds + 16 + start, s_klen[i], sp);
-    atomicOr(&s_ok[k / 32], 1u << (k % 32));
-  }
-  __syncthreads();
-  if (threadIdx.x < kSpec / 32) spec_ok[(uint64_t)blockIdx.x * (kSpec / 32) + threadIdx.x] = s_ok[threadIdx.x];
+  ev[base / kTBytes + threadIdx.x] = pk;
 }
 
 // Pass B: each thread's events (packed by pass A, or re-read from the file for a span with
 // more than kEvCap), the block scan of the span functions again (from the events: no
-// prefixes stored), the walk, the records, and every key's h1 / h2 -- the speculative
-// state when pass A computed it, else hashed from the file.  Fields are written only for
+// prefixes stored), the walk, the records, and every key's h1 / h2 -- pass A's state when
+// its slot matches the key, else hashed from the file.  Fields are written only for
 // records below min(count, cap), so a key cut off by EOF writes nothing.
 template <bool HASH>
 __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                           const GFn* __restrict__ excl, const uint64_t* __restrict__ ev,
-                                                          const uint64_t* __restrict__ spec,
-                                                          const uint32_t* __restrict__ spec_ok,
+                                                          const SpecSlot* __restrict__ spec,
                                                           const uint64_t* __restrict__ count, uint64_t cap,
                                                           k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
                                                           uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];  // overflowing spans only
-  __shared__ uint64_t s_ev[kTThreads];
-  __shared__ uint32_t s_nl[kTThreads], s_ok[kSpec / 32];
   typedef hipcub::BlockScan<LFn, kTThreads> Scan;
-  typedef hipcub::BlockScan<uint32_t, kTThreads> CScan;
   __shared__ typename Scan::TempStorage tmp;
-  __shared__ typename CScan::TempStorage ctmp;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
   const uint32_t rel = kTBytes * threadIdx.x;
   const bool live = base + rel < size;
-  const uint64_t pk = ev[(uint64_t)blockIdx.x * kTThreads + threadIdx.x];
-  const bool over = pk == kEvOverflow;
-  if (HASH && threadIdx.x < kSpec / 32) s_ok[threadIdx.x] = spec_ok[(uint64_t)blockIdx.x * (kSpec / 32) + threadIdx.x];
+  const uint64_t ti = base / kTBytes + threadIdx.x;
+  const uint64_t pk = ev[ti];
+  const bool over = ((pk >> 56) & 15u) == 15u;
+  // the slots pass A wrote for this span, loaded now so their latency hides under the scan
+  SpecSlot sl[kSlots];
+#pragma unroll
+  for (uint32_t j = 0; j < kSlots; ++j) {
+    sl[j].start = 0xFFFFFFFFu;
+    if (HASH && !over && ((pk >> (60 + j)) & 1u)) sl[j] = spec[ti * kSlots + j];
+  }
   uint8_t* span = lds + 16 + rel;
   if (over) {  // rare: stage this span's 128 bytes (bytes past the file read as 0x01)
     for (uint32_t q = 0; q < kTBytes; q += 4) {
@@ -635,54 +643,27 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
     }
   };
   FnAcc acc;
-  uint32_t nnl = 0;
-  for_events([&](uint32_t o, uint32_t t) {
-    acc.add(t, rel + o + 1);
-    nnl += t == 1u;
-  });
+  for_events([&](uint32_t o, uint32_t t) { acc.add(t, rel + o + 1); });
   LFn pre;
   Scan(tmp).ExclusiveScan(live ? acc.fn() : lfn_id(), pre, lfn_id(), LCompose());
-  uint32_t k0;
-  CScan(ctmp).ExclusiveSum(nnl, k0);
-  s_ev[threadIdx.x] = over ? kEvOverflow : pk;
-  s_nl[threadIdx.x] = k0;
-  __syncthreads();
   TState s = gapply(gfn_of(pre, base), gapply(excl[blockIdx.x], TState{0, 0, 0, 0}));
   const uint64_t lim = min(count[0], cap);
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
-  // the newline index within the block of the newline at block-relative position q, or
-  // kSpec when unknown (its span overflowed)
-  auto nl_index = [&](uint32_t q) -> uint32_t {
-    const uint32_t th = q / kTBytes, o = q % kTBytes;
-    const uint64_t w = s_ev[th];
-    if (w == kEvOverflow) return kSpec;
-    const uint32_t ne = (uint32_t)(w >> 56) & 15u;
-    uint32_t k = s_nl[th];
-    for (uint32_t j = 0; j < ne; ++j) {
-      const uint32_t e = (uint32_t)(w >> (9 * j)) & 0x1FFu;
-      if ((e & 127u) >= o) break;
-      k += (e >> 7) == 1u;
-    }
-    return k;
-  };
+  uint32_t j = 0;           // cut events of this span so far
   auto key_end = [&](uint64_t e) {
     if (s.r >= lim) return;
     recs[s.r].key_off = s.fs;
     recs[s.r].key_len = e - s.fs;
     if constexpr (HASH) {
-      uint64_t raw = 0;
-      bool got = false;
-      if (s.fs > base && s.fs - 1 < base + kTChunk) {
-        const uint32_t k = nl_index((uint32_t)(s.fs - 1 - base));
-        if (k < kSpec && ((s_ok[k / 32] >> (k % 32)) & 1u)) {
-          raw = spec[(uint64_t)blockIdx.x * kSpec + k];
-          got = true;
-        }
-      }
       uint64_t a, c;
-      if (got) {
-        a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
-        c = e > s.fs ? raw : a;
+      const uint32_t want = s.fs >= base ? (uint32_t)(s.fs - base) : 0xFFFFFFFEu;
+      const SpecSlot* hit = nullptr;
+#pragma unroll
+      for (uint32_t q = 0; q < kSlots; ++q)
+        if (j == q && sl[q].start == want) hit = &sl[q];
+      if (hit) {
+        a = hit->raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
+        c = e > s.fs ? hit->raw : a;
       } else {
         hash_cstr(f, s.fs, e - s.fs, sp, a, c);
       }
@@ -705,7 +686,9 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
         s.fs = pos + 1;
         nulf = false;
       }
-    } else if (t == 2u) {
+      return;
+    }
+    if (t == 2u) {
       if (!s.m) {  // the key getline's TAB
         if (!nulf) key_end(pos);
         s.m = 1;
@@ -717,6 +700,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
       else key_end(pos);
       nulf = true;
     }
+    ++j;
   });
   // the thread holding the last byte: a value read to EOF
   if (live && base + rel + kTBytes >= size && s.m && !nulf) val_end(size);
@@ -763,13 +747,13 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
 
 // TSV: pass A, the scan of block functions, the count, pass B (when recs), one read-back.
 // Temporaries per 16 KiB block: its function (2 x 48 B), 8 B of events per 128 B span,
-// and kSpec speculative key states + their validity bits (~2 KiB, mostly unwritten).
+// and kSlots speculative key slots per span (16 B each, written only where a key ends).
 static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
                       hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
   const uint64_t nblk = (size + kTChunk - 1) / kTChunk;
   GFn *fn = nullptr, *excl = nullptr;
-  uint64_t *dcount = nullptr, *ev = nullptr, *spec = nullptr;
-  uint32_t* spec_ok = nullptr;
+  uint64_t *dcount = nullptr, *ev = nullptr;
+  SpecSlot* spec = nullptr;
   void* tmp = nullptr;
   size_t tmp_bytes = 0;
   hipError_t e = nblk > 0x7FFFFFFFull ? hipErrorInvalidValue : hipSuccess;
@@ -781,11 +765,10 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   tr(scratch_alloc((void**)&excl, nblk * sizeof(GFn), stream));
   tr(scratch_alloc((void**)&dcount, 8, stream));
   tr(scratch_alloc((void**)&ev, nblk * kTThreads * 8, stream));
-  tr(scratch_alloc((void**)&spec, nblk * kSpec * 8, stream));
-  tr(scratch_alloc((void**)&spec_ok, nblk * (kSpec / 32) * 4, stream));
+  tr(scratch_alloc((void**)&spec, nblk * kTThreads * kSlots * sizeof(SpecSlot), stream));
   const SpadTable sp = make_spad(seed);
   if (e == hipSuccess) {
-    tsv_a_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, ev, spec, spec_ok, sp);
+    tsv_a_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, ev, spec, sp);
     e = hipGetLastError();
   }
   tr(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp_bytes, fn, excl, GCompose(), gfn_id(), nblk, stream));
@@ -797,17 +780,17 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   }
   if (e == hipSuccess && walk) {
     if (h1)
-      tsv_b_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, ev, spec, spec_ok, dcount, cap, recs,
-                                                                   sp, h1, h2);
+      tsv_b_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, ev, spec, dcount, cap, recs, sp, h1,
+                                                                   h2);
     else
-      tsv_b_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, ev, spec, spec_ok, dcount, cap,
-                                                                    recs, sp, nullptr, nullptr);
+      tsv_b_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, ev, spec, dcount, cap, recs, sp,
+                                                                    nullptr, nullptr);
     e = hipGetLastError();
   }
   uint64_t n = 0;
   tr(hipMemcpyAsync(&n, dcount, 8, hipMemcpyDeviceToHost, stream));
   tr(hipStreamSynchronize(stream));
-  for (void* p : {(void*)fn, (void*)excl, (void*)dcount, (void*)ev, (void*)spec, (void*)spec_ok, tmp})
+  for (void* p : {(void*)fn, (void*)excl, (void*)dcount, (void*)ev, (void*)spec, tmp})
     if (p) (void)hipFreeAsync(p, stream);
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;
