@@ -505,6 +505,7 @@ __device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, con
 // is in an earlier block, a third cut in one span, a span with more than kEvCap events)
 // is hashed from the file.
 constexpr uint32_t kSlots = 2;
+constexpr uint32_t kListCap = 256;  // keys hashed by pass A per block (BASELINE-like files: ~120)
 struct alignas(16) SpecSlot {
   uint64_t raw;    // FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
   uint32_t start;  // block-relative start of the key
@@ -535,9 +536,12 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
                                                           GFn* __restrict__ blk_fn, uint64_t* __restrict__ ev,
                                                           SpecSlot* __restrict__ spec, SpadTable sp) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
+  __shared__ uint64_t s_key[kListCap];  // emitted keys: start | len << 16 | slot index << 32
+  __shared__ uint32_t s_nk;
   typedef hipcub::BlockScan<ScanA, kTThreads> Scan;
   __shared__ typename Scan::TempStorage tmp;
-  tsv_stage(f, size, blockIdx.x, lds);
+  if (threadIdx.x == 0) s_nk = 0;
+  tsv_stage(f, size, blockIdx.x, lds);  // (its barrier publishes s_nk = 0)
   const uint32_t rel = kTBytes * threadIdx.x;
   const uint8_t* span = lds + 16 + rel;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
@@ -559,38 +563,42 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   Scan(tmp).ExclusiveScan(ScanA{live ? acc.fn() : lfn_id(), NlSum{live ? nl : 2u}}, pre,
                           ScanA{lfn_id(), NlSum{2u}}, ScanAOp(), agg);
   if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(agg.fn, base);
-  // keys ending at this span's cuts: the newline state entering the span, then its events
+  // keys ending at this span's cuts: the newline state entering the span, then its events;
+  // each key goes to the block's list, hashed below one lane per key
   bool open = (pre.nl.v & 3u) == 3u;
   uint32_t start = (pre.nl.v >> 2) + 1, j = 0;
-  auto emit = [&](uint32_t o, uint32_t t) {
-    const uint32_t pos = rel + o;
-    if (t == 1u) {
-      open = true;
-      start = pos + 1;
-      return;
-    }
-    if (open && j < kSlots && base + pos < size) {  // the first cut after a newline of this block
-      SpecSlot s;
-      s.raw = key_raw_lds(lds + 16 + start, pos - start, sp);
-      s.start = start;
-      s.pad = 0;
-      spec[((uint64_t)blockIdx.x * kTThreads + threadIdx.x) * kSlots + j] = s;
-      if (!over) pk |= 1ull << (60 + j);
-    }
-    open = false;
-    ++j;
-  };
-  if (live) {
-    if (over) {
-      span_events(span, emit);
-    } else {
-      for (uint32_t q = 0; q < ne; ++q) {
-        const uint32_t e = (uint32_t)(pk >> (9 * q)) & 0x1FFu;
-        emit(e & 127u, e >> 7);
+  if (live && !over) {
+    for (uint32_t q = 0; q < ne; ++q) {
+      const uint32_t e = (uint32_t)(pk >> (9 * q)) & 0x1FFu;
+      const uint32_t pos = rel + (e & 127u), t = e >> 7;
+      if (t == 1u) {
+        open = true;
+        start = pos + 1;
+        continue;
       }
+      if (open && j < kSlots && base + pos < size) {  // the first cut after a newline of this block
+        const uint32_t slot = atomicAdd(&s_nk, 1u);
+        if (slot < kListCap) {
+          s_key[slot] = start | ((uint64_t)(pos - start) << 16) | ((uint64_t)(threadIdx.x * kSlots + j) << 32);
+          pk |= 1ull << (60 + j);
+        }
+      }
+      open = false;
+      ++j;
     }
   }
   ev[base / kTBytes + threadIdx.x] = pk;
+  __syncthreads();
+  const uint32_t nk = min(s_nk, kListCap);
+  for (uint32_t i = threadIdx.x; i < nk; i += kTThreads) {
+    const uint64_t k = s_key[i];
+    const uint32_t st = (uint32_t)k & 0xFFFFu, len = (uint32_t)(k >> 16) & 0xFFFFu;
+    SpecSlot sl;
+    sl.raw = key_raw_lds(lds + 16 + st, len, sp);
+    sl.start = st;
+    sl.pad = 0;
+    spec[(uint64_t)blockIdx.x * kTThreads * kSlots + (k >> 32)] = sl;
+  }
 }
 
 // Pass B: each thread's events (packed by pass A, or re-read from the file for a span with
@@ -650,20 +658,34 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
   const uint64_t lim = min(count[0], cap);
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
   uint32_t j = 0;           // cut events of this span so far
+  // a key ended in this span whose record's value has not ended yet: its fields wait so
+  // the record is written whole (two 16-byte stores) when the value ends here too
+  uint64_t pk_r = ~0ull, pk_off = 0, pk_len = 0;
+  typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));  // recs: 8-byte aligned
+  auto flush_key = [&]() {
+    if (pk_r != ~0ull) *reinterpret_cast<u64x2*>(&recs[pk_r].key_off) = u64x2{pk_off, pk_len};
+    pk_r = ~0ull;
+  };
   auto key_end = [&](uint64_t e) {
     if (s.r >= lim) return;
-    recs[s.r].key_off = s.fs;
-    recs[s.r].key_len = e - s.fs;
+    flush_key();
+    pk_r = s.r;
+    pk_off = s.fs;
+    pk_len = e - s.fs;
     if constexpr (HASH) {
       uint64_t a, c;
       const uint32_t want = s.fs >= base ? (uint32_t)(s.fs - base) : 0xFFFFFFFEu;
-      const SpecSlot* hit = nullptr;
+      bool hit = false;
+      uint64_t raw = 0;
 #pragma unroll
       for (uint32_t q = 0; q < kSlots; ++q)
-        if (j == q && sl[q].start == want) hit = &sl[q];
+        if (j == q && sl[q].start == want) {
+          hit = true;
+          raw = sl[q].raw;
+        }
       if (hit) {
-        a = hit->raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
-        c = e > s.fs ? hit->raw : a;
+        a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
+        c = e > s.fs ? raw : a;
       } else {
         hash_cstr(f, s.fs, e - s.fs, sp, a, c);
       }
@@ -673,8 +695,13 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
   };
   auto val_end = [&](uint64_t e) {
     if (s.r >= lim) return;
-    recs[s.r].val_off = s.fs;
-    recs[s.r].val_len = e - s.fs;
+    if (pk_r == s.r) {
+      *reinterpret_cast<u64x2*>(&recs[s.r].key_off) = u64x2{pk_off, pk_len};
+      *reinterpret_cast<u64x2*>(&recs[s.r].val_off) = u64x2{s.fs, e - s.fs};
+      pk_r = ~0ull;
+    } else {
+      *reinterpret_cast<u64x2*>(&recs[s.r].val_off) = u64x2{s.fs, e - s.fs};
+    }
   };
   for_events([&](uint32_t o, uint32_t t) {
     const uint64_t pos = base + rel + o;
@@ -704,6 +731,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
   });
   // the thread holding the last byte: a value read to EOF
   if (live && base + rel + kTBytes >= size && s.m && !nulf) val_end(size);
+  flush_key();
 }
 
 }  // namespace
