@@ -505,7 +505,7 @@ __device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, con
 // is in an earlier block, a third cut in one span, a span with more than kEvCap events)
 // is hashed from the file.
 constexpr uint32_t kSlots = 2;
-constexpr uint32_t kListCap = 256;  // keys hashed by pass A per block (BASELINE-like files: ~120)
+constexpr uint32_t kListCap = 160;  // keys hashed by pass A per block (BASELINE-like files: ~120)
 struct alignas(16) SpecSlot {
   uint64_t raw;    // FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
   uint32_t start;  // block-relative start of the key
@@ -613,7 +613,6 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
                                                           const uint64_t* __restrict__ count, uint64_t cap,
                                                           k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
                                                           uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];  // overflowing spans only
   typedef hipcub::BlockScan<LFn, kTThreads> Scan;
   __shared__ typename Scan::TempStorage tmp;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
@@ -621,6 +620,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
   const bool live = base + rel < size;
   const uint64_t ti = base / kTBytes + threadIdx.x;
   const uint64_t pk = ev[ti];
+  const GFn ein = excl[blockIdx.x];
   const bool over = ((pk >> 56) & 15u) == 15u;
   // the slots pass A wrote for this span, loaded now so their latency hides under the scan
   SpecSlot sl[kSlots];
@@ -629,19 +629,45 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
     sl[j].start = 0xFFFFFFFFu;
     if (HASH && !over && ((pk >> (60 + j)) & 1u)) sl[j] = spec[ti * kSlots + j];
   }
-  uint8_t* span = lds + 16 + rel;
-  if (over) {  // rare: stage this span's 128 bytes (bytes past the file read as 0x01)
-    for (uint32_t q = 0; q < kTBytes; q += 4) {
-      uint32_t x = 0x01010101u;
-      for (uint32_t j = 0; j < 4; ++j)
-        if (base + rel + q + j < size) x = (x & ~(0xFFu << (8 * j))) | ((uint32_t)f[base + rel + q + j] << (8 * j));
-      *reinterpret_cast<uint32_t*>(span + q) = x;
+  // a span with more than kEvCap events (rare): its candidate masks from the file, each
+  // candidate's byte read back (no LDS, so the kernel keeps its occupancy)
+  uint64_t om0 = 0, om1 = 0;
+  if (over && live) {
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    uint32_t nib[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      uint32_t w[4];
+      const uint64_t o = base + rel + 16ull * q;
+      if (o + 16 <= size && (((uintptr_t)(f + o)) & 15) == 0) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(f + o);
+        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+      } else {
+        for (int k = 0; k < 4; ++k) {
+          w[k] = 0x01010101u;
+          for (int b = 0; b < 4; ++b)
+            if (o + 4 * k + b < size) w[k] = (w[k] & ~(0xFFu << (8 * b))) | ((uint32_t)f[o + 4 * k + b] << (8 * b));
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t small = ~(((w[k] & 0x7F7F7F7Fu) + 0x75757575u) | w[k]) & 0x80808080u;  // bytes < 0x0B
+        const uint32_t n4 = (small * 0x00204081u) >> 28;
+        const int word = 4 * q + k;
+        nib[word >> 3] |= n4 << (4 * (word & 7));
+      }
     }
+    om0 = nib[0] | ((uint64_t)nib[1] << 32);
+    om1 = nib[2] | ((uint64_t)nib[3] << 32);
   }
   auto for_events = [&](auto&& fn) {
     if (!live) return;
     if (over) {
-      span_events(span, fn);
+      uint64_t m0 = om0, m1 = om1;
+      for (uint32_t o = next_event(m0, m1); o < 128; o = next_event(m0, m1)) {
+        const uint32_t t = ev_type(f[base + rel + o]);
+        if (t) fn(o, t);
+      }
     } else {
       const uint32_t ne = (uint32_t)(pk >> 56) & 15u;
       for (uint32_t j = 0; j < ne; ++j) {
@@ -654,7 +680,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
   for_events([&](uint32_t o, uint32_t t) { acc.add(t, rel + o + 1); });
   LFn pre;
   Scan(tmp).ExclusiveScan(live ? acc.fn() : lfn_id(), pre, lfn_id(), LCompose());
-  TState s = gapply(gfn_of(pre, base), gapply(excl[blockIdx.x], TState{0, 0, 0, 0}));
+  TState s = gapply(gfn_of(pre, base), gapply(ein, TState{0, 0, 0, 0}));
   const uint64_t lim = min(count[0], cap);
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
   uint32_t j = 0;           // cut events of this span so far
