@@ -664,8 +664,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
     if (!live) return;
     if (over) {
       uint64_t m0 = om0, m1 = om1;
-      for (uint32_t o = next_event(m0, m1); o < 128; o = next_event(m0, m1)) {
-        const uint32_t t = ev_type(f[base + rel + o]);
+      for (uint32_t o = next_event(m0, m1); o < 128 && base + rel + o < size; o = next_event(m0, m1)) {
+        const uint32_t t = ev_type(f[base + rel + o]);  // (bytes past the file are 0x01 in the masks)
         if (t) fn(o, t);
       }
     } else {
