@@ -435,10 +435,14 @@ __global__ void tsv_count_kernel(const GFn* __restrict__ excl, const GFn* __rest
 
 // Events of a thread's span: NL / TAB / NUL bytes (types 1 / 2 / 3) in byte order.  Pass A
 // packs up to kEvCap of them into one word per thread for pass B: entry j = offset (7 bits)
-// | type << 7 at bits [9j, 9j + 9), the count at bits [56, 60); count 15 = more than kEvCap
+// | type << 7 at bits [9j, 9j + 9), the count at bits [45, 48) (7 = more than kEvCap: pass B
+// reads the span back from the file), the list index of the span's speculative keys at bits
+// [48, 56) and [56, 64) (0xFF: none; see kSlots)
 // (pass B re-reads that span from the file).
-constexpr uint32_t kEvCap = 6;
-constexpr uint64_t kEvOverflow = 15ull << 56;
+constexpr uint32_t kEvCap = 5;
+constexpr uint64_t kNoSlots = 0xFFFFull << 48;
+constexpr uint64_t kEvOverflow = (7ull << 45) | kNoSlots;
+__device__ inline uint32_t ev_count(uint64_t pk) { return (uint32_t)(pk >> 45) & 7u; }
 __device__ inline uint32_t ev_type(uint32_t c) { return c == 0x0Au ? 1u : c == 0x09u ? 2u : c == 0u ? 3u : 0u; }
 
 // The span function (positions + 1) of an event sequence: per entry mode the exit mode, the
@@ -498,14 +502,14 @@ __device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, con
 // exactly after every newline the value getline reads, and ends at the first TAB or NUL
 // after it (the key getline's TAB, or the C-string cut).  So for every cut event (TAB /
 // NUL) that is the first after a newline of the same block, pass A hashes the bytes
-// between them and stores the raw state with the key's start in the cut's slot: slot j of
-// span t = the j-th cut event of that span (j < kSlots; pk bit 60 + j marks it written).
+// between them and appends the raw state with the key's start to the block's list; the
+// j-th cut event of a span (j < kSlots) keeps the list index in its packed word.
 // Pass B, whose walk ends a key at cut event j of its span, takes the slot when the key's
 // true start equals the stored one; every other key (the file's first, a key whose newline
 // is in an earlier block, a third cut in one span, a span with more than kEvCap events)
 // is hashed from the file.
 constexpr uint32_t kSlots = 2;
-constexpr uint32_t kListCap = 160;  // keys hashed by pass A per block (BASELINE-like files: ~120)
+constexpr uint32_t kListCap = 160;  // keys hashed by pass A per block (BASELINE-like files: ~120; < 0xFF)
 struct alignas(16) SpecSlot {
   uint64_t raw;    // FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
   uint32_t start;  // block-relative start of the key
@@ -558,7 +562,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
       else nl &= ~2u;
     });
   const bool over = ne > kEvCap;
-  pk = over ? kEvOverflow : pk | ((uint64_t)ne << 56);
+  pk = over ? kEvOverflow : pk | ((uint64_t)ne << 45) | kNoSlots;
   ScanA pre, agg;
   Scan(tmp).ExclusiveScan(ScanA{live ? acc.fn() : lfn_id(), NlSum{live ? nl : 2u}}, pre,
                           ScanA{lfn_id(), NlSum{2u}}, ScanAOp(), agg);
@@ -579,8 +583,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
       if (open && j < kSlots && base + pos < size) {  // the first cut after a newline of this block
         const uint32_t slot = atomicAdd(&s_nk, 1u);
         if (slot < kListCap) {
-          s_key[slot] = start | ((uint64_t)(pos - start) << 16) | ((uint64_t)(threadIdx.x * kSlots + j) << 32);
-          pk |= 1ull << (60 + j);
+          s_key[slot] = start | ((uint64_t)(pos - start) << 16);
+          pk = (pk & ~(0xFFull << (48 + 8 * j))) | ((uint64_t)slot << (48 + 8 * j));
         }
       }
       open = false;
@@ -597,7 +601,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     sl.raw = key_raw_lds(lds + 16 + st, len, sp);
     sl.start = st;
     sl.pad = 0;
-    spec[(uint64_t)blockIdx.x * kTThreads * kSlots + (k >> 32)] = sl;
+    spec[(uint64_t)blockIdx.x * kListCap + i] = sl;
   }
 }
 
@@ -621,13 +625,14 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
   const uint64_t ti = base / kTBytes + threadIdx.x;
   const uint64_t pk = ev[ti];
   const GFn ein = excl[blockIdx.x];
-  const bool over = ((pk >> 56) & 15u) == 15u;
+  const bool over = ev_count(pk) == 7u;
   // the slots pass A wrote for this span, loaded now so their latency hides under the scan
   SpecSlot sl[kSlots];
 #pragma unroll
   for (uint32_t j = 0; j < kSlots; ++j) {
     sl[j].start = 0xFFFFFFFFu;
-    if (HASH && !over && ((pk >> (60 + j)) & 1u)) sl[j] = spec[ti * kSlots + j];
+    const uint32_t li = (uint32_t)(pk >> (48 + 8 * j)) & 0xFFu;
+    if (HASH && li != 0xFFu) sl[j] = spec[(uint64_t)blockIdx.x * kListCap + li];
   }
   // a span with more than kEvCap events (rare): its candidate masks from the file, each
   // candidate's byte read back (no LDS, so the kernel keeps its occupancy)
@@ -669,7 +674,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
         if (t) fn(o, t);
       }
     } else {
-      const uint32_t ne = (uint32_t)(pk >> 56) & 15u;
+      const uint32_t ne = ev_count(pk);
       for (uint32_t j = 0; j < ne; ++j) {
         const uint32_t e = (uint32_t)(pk >> (9 * j)) & 0x1FFu;
         fn(e & 127u, e >> 7);
@@ -801,7 +806,7 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
 
 // TSV: pass A, the scan of block functions, the count, pass B (when recs), one read-back.
 // Temporaries per 16 KiB block: its function (2 x 48 B), 8 B of events per 128 B span,
-// and kSlots speculative key slots per span (16 B each, written only where a key ends).
+// and the block's list of speculative key states (16 B each, up to kListCap).
 static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
                       hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
   const uint64_t nblk = (size + kTChunk - 1) / kTChunk;
@@ -819,7 +824,7 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   tr(scratch_alloc((void**)&excl, nblk * sizeof(GFn), stream));
   tr(scratch_alloc((void**)&dcount, 8, stream));
   tr(scratch_alloc((void**)&ev, nblk * kTThreads * 8, stream));
-  tr(scratch_alloc((void**)&spec, nblk * kTThreads * kSlots * sizeof(SpecSlot), stream));
+  tr(scratch_alloc((void**)&spec, nblk * kListCap * sizeof(SpecSlot), stream));
   const SpadTable sp = make_spad(seed);
   if (e == hipSuccess) {
     tsv_a_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, ev, spec, sp);
