@@ -804,34 +804,64 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
   return pools[dev] ? hipMallocFromPoolAsync(p, bytes, pools[dev], stream) : hipMallocAsync(p, bytes, stream);
 }
 
+// The TSV temporaries, one grow-only buffer per device held across calls (under a
+// per-device lock for the call) while it stays within kScratchKeep: per-call pool
+// allocations of this size cost ~0.15 ms per hipFreeAsync on MI355X (rocprofv3
+// --runtime-trace, profiles/r03f_import_api_stats.csv), more than the scan itself.
+struct TsvScratch {
+  std::mutex mu;
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+TsvScratch g_tsv[64];
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
 // TSV: pass A, the scan of block functions, the count, pass B (when recs), one read-back.
 // Temporaries per 16 KiB block: its function (2 x 48 B), 8 B of events per 128 B span,
 // and the block's list of speculative key states (16 B each, up to kListCap).
 static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
                       hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
   const uint64_t nblk = (size + kTChunk - 1) / kTChunk;
-  GFn *fn = nullptr, *excl = nullptr;
-  uint64_t *dcount = nullptr, *ev = nullptr;
-  SpecSlot* spec = nullptr;
-  void* tmp = nullptr;
-  size_t tmp_bytes = 0;
   hipError_t e = nblk > 0x7FFFFFFFull ? hipErrorInvalidValue : hipSuccess;
   auto tr = [&](hipError_t x) {
     if (e == hipSuccess) e = x;
   };
+  int dev = 0;
+  tr(hipGetDevice(&dev));
+  if (e == hipSuccess && (dev < 0 || dev >= 64)) e = hipErrorInvalidDevice;
+  if (e != hipSuccess) {
+    *herr = e;
+    return K2H_AMD_EHIP;
+  }
+  size_t tmp_bytes = 0;
+  tr(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp_bytes, (GFn*)nullptr, (GFn*)nullptr, GCompose(), gfn_id(), nblk,
+                                       stream));
+  const size_t o_fn = 0, o_excl = o_fn + align256(nblk * sizeof(GFn)), o_cnt = o_excl + align256(nblk * sizeof(GFn));
+  const size_t o_ev = o_cnt + 256, o_spec = o_ev + align256(nblk * kTThreads * 8);
+  const size_t o_tmp = o_spec + align256(nblk * kListCap * sizeof(SpecSlot)), total = o_tmp + align256(tmp_bytes + 1);
+  TsvScratch& sc = g_tsv[dev];
+  std::lock_guard<std::mutex> lk(sc.mu);
+  if (e == hipSuccess && sc.bytes < total) {
+    if (sc.p) tr(hipFree(sc.p));
+    sc.p = nullptr;
+    sc.bytes = 0;
+    tr(hipMalloc(&sc.p, total));
+    if (e == hipSuccess) sc.bytes = total;
+  }
+  uint8_t* base = (uint8_t*)sc.p;
+  GFn* fn = (GFn*)(base + o_fn);
+  GFn* excl = (GFn*)(base + o_excl);
+  uint64_t* dcount = (uint64_t*)(base + o_cnt);
+  uint64_t* ev = (uint64_t*)(base + o_ev);
+  SpecSlot* spec = (SpecSlot*)(base + o_spec);
+  void* tmp = base + o_tmp;
   const bool walk = recs && cap;
-  tr(scratch_alloc((void**)&fn, nblk * sizeof(GFn), stream));
-  tr(scratch_alloc((void**)&excl, nblk * sizeof(GFn), stream));
-  tr(scratch_alloc((void**)&dcount, 8, stream));
-  tr(scratch_alloc((void**)&ev, nblk * kTThreads * 8, stream));
-  tr(scratch_alloc((void**)&spec, nblk * kListCap * sizeof(SpecSlot), stream));
   const SpadTable sp = make_spad(seed);
   if (e == hipSuccess) {
     tsv_a_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, ev, spec, sp);
     e = hipGetLastError();
   }
-  tr(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp_bytes, fn, excl, GCompose(), gfn_id(), nblk, stream));
-  tr(scratch_alloc(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
   tr(hipcub::DeviceScan::ExclusiveScan(tmp, tmp_bytes, fn, excl, GCompose(), gfn_id(), nblk, stream));
   if (e == hipSuccess) {
     tsv_count_kernel<<<1, 1, 0, stream>>>(excl, fn, nblk, dcount);
@@ -849,8 +879,11 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   uint64_t n = 0;
   tr(hipMemcpyAsync(&n, dcount, 8, hipMemcpyDeviceToHost, stream));
   tr(hipStreamSynchronize(stream));
-  for (void* p : {(void*)fn, (void*)excl, (void*)dcount, (void*)ev, (void*)spec, tmp})
-    if (p) (void)hipFreeAsync(p, stream);
+  if (sc.bytes > kScratchKeep) {  // the stream is synchronised: no kernel still reads it
+    (void)hipFree(sc.p);
+    sc.p = nullptr;
+    sc.bytes = 0;
+  }
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;
   *count = n;
