@@ -16,11 +16,10 @@
 //   80 i + sum over segments of (seg_off[i] - seg_off[0])
 // and no scan is needed.
 //
-// One kernel (ralledata_gather_kernel<true>, below): tiles of 64 records staged in LDS,
-// the keys hashed there, the blobs written as aligned 16-byte pieces; tiles too large to
-// stage run the 8-lane group form inside the same kernel.  The lab build keeps the round-1
-// two-kernel forms (CSR hash into scratch, then a group / thread / LDS-image assembly) as
-// A/B variants.  Blob and segment addresses are byte-aligned.
+// One kernel (ralledata_gather_kernel, below): tiles of 64 records staged in LDS, the keys
+// hashed there, the blobs written as aligned 16-byte pieces; tiles too large to stage run
+// the 8-lane group form inside the same kernel.  Blob and segment addresses are
+// byte-aligned.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -37,64 +36,27 @@ __device__ __forceinline__ uint64_t seg_len(const uint64_t* off, uint64_t i) { r
 __device__ __forceinline__ uint64_t seg_before(const uint64_t* off, uint64_t i) { return off ? off[i] - off[0] : 0; }
 
 
-// Group form (default): G lanes per record, 64/G records per wave.  Lane q of a group
+// Group form (oversize tiles): G lanes per record, 64/G records per wave.  Lane q of a group
 // writes header piece q (5 x 16 B) and copies bytes [16q + 16Gj, +16) of each segment,
 // so a group's loads and stores are consecutive 16-byte pieces instead of one lane
 // streaming a whole record.  A segment's last partial piece is the 16 bytes ENDING at
 // its last byte (they overlap the previous piece with the same bytes, so the order of
 // the two stores does not matter); only segments shorter than 16 bytes are copied byte
 // by byte.  G = 8 keeps most lanes busy on BASELINE-like records (keys 8-64 B, values
-// 0-256 B); G = 16 and the round-1 byte-tail form are A/B variants.
-template <int G, bool BYTE_TAIL = false, int PROBE = 0>
+// 0-256 B).
+template <int G>
 __device__ __forceinline__ void group_copy(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint64_t len,
                                            uint32_t q) {
-  if constexpr (PROBE == 1) dst = (uint8_t*)((uintptr_t)dst & ~(uintptr_t)15);  // timing probe: aligned stores
   uint64_t full = len & ~15ull;
   for (uint64_t j = 16ull * q; j < full; j += 16ull * G)
     *reinterpret_cast<u32x4_ua*>(dst + j) = *reinterpret_cast<const u32x4_ua*>(src + j);
   if (full == len) return;
-  if (!BYTE_TAIL && len >= 16) {
+  if (len >= 16) {
     if (q == G - 1)
       *reinterpret_cast<u32x4_ua*>(dst + len - 16) = *reinterpret_cast<const u32x4_ua*>(src + len - 16);
     return;
   }
   for (uint64_t t = full + q; t < len; t += G) dst[t] = src[t];  // the <= 15 tail bytes
-}
-
-// PROBE (timing only, wrong blobs): 1 = segment stores 16-byte aligned, 2 = no segment copies.
-template <int G, bool BYTE_TAIL = false, int PROBE = 0>
-__global__ __launch_bounds__(256) void ralledata_group_kernel(RalleInputs in, uint64_t n, const uint64_t* __restrict__ h,
-                                                              uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off) {
-  static_assert(G >= 5 && 64 % G == 0, "five lanes write the header");
-  const uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) / G;
-  const uint32_t q = threadIdx.x % G;
-  if (i >= n) return;
-  const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i), al = seg_len(in.aoff, i);
-  const uint64_t o = 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) +
-                     seg_before(in.aoff, i);
-  uint8_t* b = out + o;
-  if (q < 5) {
-    uint64_t f0, f1;
-    switch (q) {
-      case 0: f0 = h[i]; f1 = h[n + i]; break;
-      case 1: f0 = kl; f1 = vl; break;
-      case 2: f0 = sl; f1 = al; break;
-      case 3: f0 = 80; f1 = 80 + kl; break;
-      default: f0 = 80 + kl + vl; f1 = 80 + kl + vl + sl; break;
-    }
-    *reinterpret_cast<u32x4_ua*>(b + 16 * q) =
-        u32x4_ua{(uint32_t)f0, (uint32_t)(f0 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32)};
-  }
-  if constexpr (PROBE != 2) {
-    if (kl) group_copy<G, BYTE_TAIL, PROBE>(b + 80, in.keys + in.koff[i], kl, q);
-    if (vl) group_copy<G, BYTE_TAIL, PROBE>(b + 80 + kl, in.vals + in.voff[i], vl, q);
-    if (sl) group_copy<G, BYTE_TAIL, PROBE>(b + 80 + kl + vl, in.skeys + in.soff[i], sl, q);
-    if (al) group_copy<G, BYTE_TAIL, PROBE>(b + 80 + kl + vl + sl, in.attrs + in.aoff[i], al, q);
-  }
-  if (blob_off && q == 0) {
-    blob_off[i] = o;
-    if (i + 1 == n) blob_off[n] = o + 80 + kl + vl + sl + al;
-  }
 }
 
 // Gather form (round 2): output-driven.  A block takes R consecutive records; its blobs are
@@ -141,12 +103,11 @@ __device__ __forceinline__ void global_key_hash(const uint8_t* keys, uint64_t b,
   r2 = k ? (len == 1 ? r1 : ((uint64_t)hi2 << 32) | lo2) : 0;
 }
 
-// one record by a group of G lanes, straight to HBM (the group form); HASH: lane 0 hashes
-// the key itself instead of reading h
-template <int G, bool HASH = false>
-__device__ __forceinline__ void group_record(const RalleInputs& in, uint64_t n, const uint64_t* __restrict__ h,
-                                             uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off,
-                                             uint64_t i, uint32_t q, const uint64_t* spad = nullptr) {
+// one record by a group of G lanes, straight to HBM (the group form); lane 0 hashes the key
+template <int G>
+__device__ __forceinline__ void group_record(const RalleInputs& in, uint64_t n, uint8_t* __restrict__ out,
+                                             uint64_t* __restrict__ blob_off, uint64_t i, uint32_t q,
+                                             const uint64_t* spad) {
   const uint64_t kl = seg_len(in.koff, i), vl = seg_len(in.voff, i), sl = seg_len(in.soff, i), al = seg_len(in.aoff, i);
   const uint64_t o = 80ull * i + seg_before(in.koff, i) + seg_before(in.voff, i) + seg_before(in.soff, i) +
                      seg_before(in.aoff, i);
@@ -155,13 +116,8 @@ __device__ __forceinline__ void group_record(const RalleInputs& in, uint64_t n, 
     uint64_t f0, f1;
     switch (q) {
       case 0:
-        if constexpr (HASH) {
-          if (in.koff) global_key_hash(in.keys, in.koff[i], in.koff[i + 1], spad, f0, f1);
-          else f0 = f1 = 0;
-        } else {
-          f0 = h[i];
-          f1 = h[n + i];
-        }
+        if (in.koff) global_key_hash(in.keys, in.koff[i], in.koff[i + 1], spad, f0, f1);
+        else f0 = f1 = 0;
         break;
       case 1: f0 = kl; f1 = vl; break;
       case 2: f0 = sl; f1 = al; break;
@@ -180,7 +136,7 @@ __device__ __forceinline__ void group_record(const RalleInputs& in, uint64_t n, 
   }
 }
 
-// Key hash from the staged bytes (FUSED): end-aligned 16-byte chunks (the CSR kernels'
+// Key hash from the staged bytes: end-aligned 16-byte chunks (the CSR kernels'
 // scheme): chunk 0 starts 16k - len bytes early with those bytes
 // zeroed and the state started at S_p = seed * P^-p, so no byte tail; the last chunk's
 // byte 15 step leaves the second hash (the state before the last byte).
@@ -204,20 +160,11 @@ __device__ __forceinline__ void staged_key_hash(const uint8_t* end, uint32_t len
   r2 = k ? (len == 1 ? r1 : ((uint64_t)hi2 << 32) | lo2) : 0;
 }
 
-// FUSED: the key hashes are computed here from the staged key bytes (no hash kernel, no
-// scratch); otherwise h holds h1[n] then h2[n] from the CSR hash kernel.  PROBE (lab,
-// tools/ralle_phases.py): thread 0 overwrites blob_off[r0 .. r0+5] with shader-clock
-// stamps (entry, span offsets in, records done, after each barrier, end of its pieces;
-// wrong offsets), 2: the same without the piece stores.  PU: pieces per loop trip;
-// SW0: the staged loads on all four waves (default: waves 1-3, so wave 0 only waits for its
-// records' offsets)
-// PRIO (lab): 1 = the loads (record offsets, span offsets, staged pieces) issued at raised
-// issue priority; 2 = all of phase 1 (loads and record work) at raised priority.
-template <bool FUSED, int PROBE = 0, int PU = 1, bool SW0 = false, int PRIO = 0>
+// The key hashes are computed here from the staged keys (no hash kernel, no scratch).
+// Wave 0 only waits for its records' offsets (the staged loads are issued by waves 1-3).
 // 7 waves/SIMD (<= 72 VGPRs): the LDS image allows 7 blocks per CU
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void ralledata_gather_kernel(
-    RalleInputs in, uint64_t n, const uint64_t* __restrict__ h, uint8_t* __restrict__ out,
-    uint64_t* __restrict__ blob_off, SpadTable spad_tab) {
+    RalleInputs in, uint64_t n, uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off, SpadTable spad_tab) {
   constexpr int R = kGatherRecs, NSEG = 5 * R;
   typedef uint32_t u32x4_al __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) uint8_t img[kGatherImg];
@@ -226,9 +173,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
   __shared__ u32x4_al qmask[17];
   __shared__ uint64_t spad[16];
   const uint32_t tid = threadIdx.x;
-  uint64_t t0 = 0, t1 = 0, t2 = 0, ta = 0, tb = 0;
-  if constexpr (PROBE) t0 = __builtin_amdgcn_s_memtime();
-  if constexpr (PRIO) __builtin_amdgcn_s_setprio(1);
   const uint64_t r0 = (uint64_t)blockIdx.x * R;
   const uint32_t nr = (uint32_t)(n - r0 < (uint64_t)R ? n - r0 : (uint64_t)R);
   const uint64_t* offs[4] = {in.koff, in.voff, in.soff, in.aoff};
@@ -264,21 +208,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
     hull_total += hull_n[s];
   }
   if (16 * hull_total > (uint64_t)kGatherPool) {  // block-uniform: too large to stage
-    if constexpr (FUSED) {
-      // hash then assemble: the group form reads the hashes back from this block's records
-      // (one lane per record, straight from HBM, written to the blobs' first 16 bytes below)
-      if (tid < 16) spad[tid] = spad_tab.v[tid];
-      __syncthreads();
-      for (uint32_t rec = tid / 8; rec < nr; rec += 32) group_record<8, true>(in, n, nullptr, out, blob_off, r0 + rec, tid % 8, spad);
-    } else {
-      for (uint32_t rec = tid / 8; rec < nr; rec += 32) group_record<8>(in, n, h, out, blob_off, r0 + rec, tid % 8);
-    }
+    // the group form, one record per 8 lanes straight to HBM, lane 0 hashing the key
+    if (tid < 16) spad[tid] = spad_tab.v[tid];
+    __syncthreads();
+    for (uint32_t rec = tid / 8; rec < nr; rec += 32) group_record<8>(in, n, out, blob_off, r0 + rec, tid % 8, spad);
     return;
   }
-  if constexpr (PROBE != 0) ta = __builtin_amdgcn_s_memtime();  // span offsets arrived
   // 1a. the staged pieces: up to 4 aligned loads per thread of waves 1-3 (wave 0's only
   // loads are its records' offsets, so its record work waits for nothing else)
-  constexpr uint32_t SW = SW0 ? 0 : 64, NST = 256 - SW;
+  constexpr uint32_t SW = 64, NST = 256 - SW;
   constexpr int PPT = (kGatherPool / 16 + NST - 1) / NST;
   u32x4_al v[PPT];
   uint32_t dst[PPT];
@@ -297,7 +235,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
       dst[u] = kGatherHdr + 80 * R + 16 * (uint32_t)q;
     }
   }
-  if constexpr (PRIO == 1) __builtin_amdgcn_s_setprio(0);
   // 1b. one thread per record: header, segment table, piece table, blob offset.  All
   // block-relative quantities fit 32 bits once the spans fit the image.
   const uint64_t a_out = (uint64_t)(uintptr_t)(out + o_first);
@@ -310,7 +247,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
     m.w = (uint32_t)(~0ull << (8 * min(max((int)tid - 12, 0), 4)));
     qmask[tid] = m;
   }
-  if (FUSED && tid < 16) spad[tid] = spad_tab.v[tid];
+  if (tid < 16) spad[tid] = spad_tab.v[tid];
   if (tid < nr) {
     const uint64_t i = r0 + tid;
     uint32_t rel[4], len[4];
@@ -321,12 +258,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
     }
     const int32_t B = (int32_t)(80u * tid + rel[0] + rel[1] + rel[2] + rel[3]);
     const uint32_t kl = len[0], vl = len[1], sl = len[2], al = len[3];
-    uint64_t h1 = 0, h2 = 0;
-    if constexpr (!FUSED) {
-      h1 = h[i];
-      h2 = h[n + i];
-    }
-    const uint32_t f[20] = {(uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32), kl, 0, vl, 0, sl, 0,
+    const uint32_t f[20] = {0, 0, 0, 0, kl, 0, vl, 0, sl, 0,  // hashes: filled in by wave 0 below
                             al, 0, 80, 0, 80 + kl, 0, 80 + kl + vl, 0, 80 + kl + vl + sl, 0};
 #pragma unroll
     for (int c = 0; c < 5; ++c)
@@ -348,24 +280,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
       if (i + 1 == n) blob_off[n] = o_first + start;
     }
   }
-  if constexpr (PROBE != 0) tb = __builtin_amdgcn_s_memtime();  // records done (thread 0)
 #pragma unroll
   for (int u = 0; u < PPT; ++u)
     if (dst[u] != 0xffffffffu) *reinterpret_cast<u32x4_al*>(img + dst[u]) = v[u];
-  if constexpr (PRIO == 2) __builtin_amdgcn_s_setprio(0);
   __syncthreads();
-  if constexpr (PROBE) t1 = __builtin_amdgcn_s_memtime();
-  if constexpr (FUSED) {  // 1c. wave 0 hashes the block's keys from the image into the headers
-    if (tid < nr) {
-      const uint32_t kl = ro1[0] - ro0[0], ke = ro1[0] - (uint32_t)sbase[0];
-      uint64_t h1, h2;
-      staged_key_hash(img + area[0] + ke, kl, spad, h1, h2);
-      *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid) =
-          u32x4_al{(uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32)};
-    }
-    __syncthreads();
+  // 1c. wave 0 hashes the block's keys from the image into the headers
+  if (tid < nr) {
+    const uint32_t kl = ro1[0] - ro0[0], ke = ro1[0] - (uint32_t)sbase[0];
+    uint64_t h1, h2;
+    staged_key_hash(img + area[0] + ke, kl, spad, h1, h2);
+    *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid) =
+        u32x4_al{(uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32)};
   }
-  if constexpr (PROBE) t2 = __builtin_amdgcn_s_memtime();
+  __syncthreads();
   // 2. aligned output pieces: the window of each segment in the piece, aligned with the
   // piece, merged forward (segment k supplies bytes [its start, 16) over what came before)
   const int32_t sp = (int32_t)span;
@@ -398,9 +325,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
         }
       }
     }
-    if (PROBE == 2) {
-      if (acc.x == 0x9e3779b9u && acc.y == p) base[0] = 0;  // keep the gather, drop the stores
-    } else if (x >= 0 && x + 16 <= sp) {
+    if (x >= 0 && x + 16 <= sp) {
       __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_al*>(base + 16ull * p));
     } else {  // shared with a neighbouring block: this block's bytes only
       const uint32_t wv[4] = {acc.x, acc.y, acc.z, acc.w};
@@ -414,32 +339,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
     const int32_t at = min(max(sg.x + 16 * (int32_t)p - d0, 0), kGatherImg - 16);
     return *reinterpret_cast<const u32x4_ua*>(img + at);
   };
-  if constexpr (PU == 2) {  // two pieces per trip: their LDS reads in flight together
-    for (uint32_t p = tid; p < np; p += 512) {
-      const uint32_t q = p + 256 < np ? p + 256 : p;
-      const uint32_t ga = tab[p], gb = tab[q];
-      const int2 a0 = seg[ga], a1 = seg[ga + 1], b0 = seg[gb], b1 = seg[gb + 1];
-      const u32x4_ua wa0 = window(a0, p), wa1 = window(a1, p), wb0 = window(b0, q), wb1 = window(b1, q);
-      piece(p, ga, a0, a1, wa0, wa1);
-      if (q != p) piece(q, gb, b0, b1, wb0, wb1);
-    }
-  } else {
-    for (uint32_t p = tid; p < np; p += 256) {
-      const uint32_t g = tab[p];
-      const int2 s0 = seg[g], s1 = seg[g + 1];  // the piece's segment and the next, one read
-      piece(p, g, s0, s1, window(s0, p), window(s1, p));
-    }
-  }
-  if constexpr (PROBE != 0) {
-    const uint64_t t3 = __builtin_amdgcn_s_memtime();
-    if (tid == 0 && nr >= 6) {
-      blob_off[r0] = t0;
-      blob_off[r0 + 1] = t1;
-      blob_off[r0 + 2] = t2;
-      blob_off[r0 + 3] = t3;
-      blob_off[r0 + 4] = ta;
-      blob_off[r0 + 5] = tb;
-    }
+  for (uint32_t p = tid; p < np; p += 256) {
+    const uint32_t g = tab[p];
+    const int2 s0 = seg[g], s1 = seg[g + 1];  // the piece's segment and the next, one read
+    piece(p, g, s0, s1, window(s0, p), window(s1, p));
   }
 }
 
@@ -452,8 +355,8 @@ hipError_t launch_ralledata(const RalleInputs& in, uint64_t n, uint64_t seed, ui
     return hipSuccess;
   }
   // one kernel, the key hashes computed from the staged keys
-  ralledata_gather_kernel<true>
-      <<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, nullptr, out, blob_off, make_spad(seed));
+  ralledata_gather_kernel<<<(unsigned)((n + kGatherRecs - 1) / kGatherRecs), 256, 0, stream>>>(in, n, out, blob_off,
+                                                                                                make_spad(seed));
   return hipGetLastError();
 }
 
