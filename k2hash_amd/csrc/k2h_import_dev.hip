@@ -425,14 +425,6 @@ __device__ inline uint32_t next_event(uint64_t& m0, uint64_t& m1) {
   return b;
 }
 
-// Record count: the whole file's function from the start state, plus the record a
-// value getline ends at EOF.
-__global__ void tsv_count_kernel(const GFn* __restrict__ excl, const GFn* __restrict__ blk_fn, uint64_t nblk,
-                                 uint64_t* __restrict__ out) {
-  const TState e = gapply(GCompose()(excl[nblk - 1], blk_fn[nblk - 1]), TState{0, 0, 0, 0});
-  out[0] = e.r + e.m;
-}
-
 // Events of a thread's span: NL / TAB / NUL bytes (types 1 / 2 / 3) in byte order.  Pass A
 // packs up to kEvCap of them into one word per thread for pass B: entry j = offset (7 bits)
 // | type << 7 at bits [9j, 9j + 9), the count at bits [45, 48) (7 = more than kEvCap: pass B
@@ -510,10 +502,11 @@ __device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, con
 // is hashed from the file.
 constexpr uint32_t kSlots = 2;
 constexpr uint32_t kListCap = 160;  // keys hashed by pass A per block (BASELINE-like files: ~120; < 0xFF)
-struct alignas(16) SpecSlot {
-  uint64_t raw;    // FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
-  uint32_t start;  // block-relative start of the key
-  uint32_t pad;
+// A block's list is two arrays at the same index: the FNV state after the key's bytes (h2
+// of key + NUL; h1 = raw * P) and the key's block-relative start (10 bytes per key).
+struct SpecList {
+  uint64_t* raw;     // [nblk * kListCap]
+  uint16_t* start;   // [nblk * kListCap]
 };
 
 // Newline state of a span for the speculative keys: whether it holds a newline, whether
@@ -534,15 +527,69 @@ struct ScanAOp {
   __device__ ScanA operator()(const ScanA& x, const ScanA& y) const { return ScanA{LCompose()(x.fn, y.fn), nl_compose(x.nl, y.nl)}; }
 };
 
-// Pass A: each block's function (for the device scan), each thread's packed events, and
+// Entry states of the blocks (tsv_scan_kernel, one launch instead of a device scan and a
+// count kernel): blocks form tiles of kTile, each tile scanned by one block into each
+// block's in-tile prefix; the last tile to finish scans the tile functions into each
+// tile's entry state and the record count (the state after the whole file, plus the
+// record a value getline ends at EOF).  The counter is zero between calls: the last
+// block resets it.
+constexpr uint32_t kTilePer = 4;
+constexpr uint32_t kTile = kTilePer * kTThreads;  // blocks per tile
+struct EntryScan {
+  GFn* blk_fn;         // [nblk] each block's function
+  GFn* intile;         // [nblk] exclusive prefix of its function within its tile
+  GFn* tile_fn;        // [ntile]
+  TState* tile_in;     // [ntile] state entering the tile
+  uint32_t* done;      // tiles finished, zero between calls
+  uint64_t* count;     // records in the file
+  uint64_t nblk, ntile;
+};
+
+// Exclusive scan of in[0, n) by one block, thread t owning the run [t k, (t + 1) k):
+// out(i, prefix of in[0, i)); returns the whole reduction.  Runs of up to 4 are loaded
+// at once and kept in registers (the tile scan's 4 and the tile-level scan of files up to
+// 4 GiB); longer runs re-read their elements.
+template <class Tmp, class Out>
+__device__ inline GFn block_scan_runs(Tmp& tmp, const GFn* in, uint64_t n, uint64_t k, Out&& out) {
+  typedef hipcub::BlockScan<GFn, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> GScan;
+  const uint64_t i0 = (uint64_t)threadIdx.x * k, i1 = min(i0 + k, n);
+  GFn x[4];
+  GFn loc = gfn_id();
+  if (k <= 4) {
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) x[q] = i0 + q < i1 ? in[i0 + q] : gfn_id();
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) loc = GCompose()(loc, x[q]);
+  } else {
+    for (uint64_t i = i0; i < i1; ++i) loc = GCompose()(loc, in[i]);
+  }
+  GFn pre, agg;
+  GScan(tmp).ExclusiveScan(loc, pre, gfn_id(), GCompose(), agg);
+  if (k <= 4) {
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q)
+      if (i0 + q < i1) {
+        out(i0 + q, pre);
+        pre = GCompose()(pre, x[q]);
+      }
+  } else {
+    for (uint64_t i = i0; i < i1; ++i) {
+      out(i, pre);
+      pre = GCompose()(pre, in[i]);
+    }
+  }
+  return agg;
+}
+
+// Pass A: each block's function (for tsv_scan_kernel), each thread's packed events, and
 // the speculative key states.
 __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                           GFn* __restrict__ blk_fn, uint64_t* __restrict__ ev,
-                                                          SpecSlot* __restrict__ spec, SpadTable sp) {
+                                                          SpecList spec, SpadTable sp) {
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
   __shared__ uint64_t s_key[kListCap];  // emitted keys: start | len << 16 | slot index << 32
   __shared__ uint32_t s_nk;
-  typedef hipcub::BlockScan<ScanA, kTThreads> Scan;
+  typedef hipcub::BlockScan<ScanA, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> Scan;
   __shared__ typename Scan::TempStorage tmp;
   if (threadIdx.x == 0) s_nk = 0;
   tsv_stage(f, size, blockIdx.x, lds);  // (its barrier publishes s_nk = 0)
@@ -597,11 +644,39 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   for (uint32_t i = threadIdx.x; i < nk; i += kTThreads) {
     const uint64_t k = s_key[i];
     const uint32_t st = (uint32_t)k & 0xFFFFu, len = (uint32_t)(k >> 16) & 0xFFFFu;
-    SpecSlot sl;
-    sl.raw = key_raw_lds(lds + 16 + st, len, sp);
-    sl.start = st;
-    sl.pad = 0;
-    spec[(uint64_t)blockIdx.x * kListCap + i] = sl;
+    spec.raw[(uint64_t)blockIdx.x * kListCap + i] = key_raw_lds(lds + 16 + st, len, sp);
+    spec.start[(uint64_t)blockIdx.x * kListCap + i] = (uint16_t)st;
+  }
+}
+
+// The entry-state scan between the passes, one block per tile: the tile's functions into
+// each block's in-tile prefix; the last tile to finish (an arrival counter) scans the tile
+// functions into each tile's entry state and the record count.  (Inside pass A this cost
+// 3.4 ms instead of 0.45: an agent-scope release per 16 KiB block writes back the XCD's
+// L2 each time, r03i.)
+__global__ __launch_bounds__(kTThreads) void tsv_scan_kernel(EntryScan es) {
+  typedef hipcub::BlockScan<GFn, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> GScan;
+  __shared__ typename GScan::TempStorage gtmp;
+  __shared__ uint32_t s_last;
+  const uint64_t tile = blockIdx.x, b0 = tile * kTile;
+  const GFn tf = block_scan_runs(gtmp, es.blk_fn + b0, min<uint64_t>(kTile, es.nblk - b0), kTilePer,
+                                 [&](uint64_t i, const GFn& p) { es.intile[b0 + i] = p; });
+  if (threadIdx.x == 0) {
+    es.tile_fn[tile] = tf;
+    __threadfence();
+    s_last = atomicAdd(es.done, 1u) == es.ntile - 1;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();  // acquire: every tile's function
+  const uint64_t k = (es.ntile + kTThreads - 1) / kTThreads;
+  const TState s0{0, 0, 0, 0};
+  const GFn all = block_scan_runs(gtmp, es.tile_fn, es.ntile, k,
+                                  [&](uint64_t i, const GFn& p) { es.tile_in[i] = gapply(p, s0); });
+  if (threadIdx.x == 0) {
+    const TState e = gapply(all, s0);
+    es.count[0] = e.r + e.m;
+    es.done[0] = 0;
   }
 }
 
@@ -612,8 +687,11 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
 // records below min(count, cap), so a key cut off by EOF writes nothing.
 template <bool HASH>
 __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                          const GFn* __restrict__ excl, const uint64_t* __restrict__ ev,
-                                                          const SpecSlot* __restrict__ spec,
+                                                          const GFn* __restrict__ intile,
+                                                          const TState* __restrict__ tile_in,
+                                                          const uint64_t* __restrict__ ev,
+                                                          const uint64_t* __restrict__ spec_raw,
+                                                          const uint16_t* __restrict__ spec_start,
                                                           const uint64_t* __restrict__ count, uint64_t cap,
                                                           k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
                                                           uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
@@ -624,15 +702,21 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
   const bool live = base + rel < size;
   const uint64_t ti = base / kTBytes + threadIdx.x;
   const uint64_t pk = ev[ti];
-  const GFn ein = excl[blockIdx.x];
+  const GFn ein = intile[blockIdx.x];
+  const TState tin = tile_in[blockIdx.x / kTile];
   const bool over = ev_count(pk) == 7u;
   // the slots pass A wrote for this span, loaded now so their latency hides under the scan
-  SpecSlot sl[kSlots];
+  uint64_t sl_raw[kSlots];
+  uint32_t sl_start[kSlots];
 #pragma unroll
   for (uint32_t j = 0; j < kSlots; ++j) {
-    sl[j].start = 0xFFFFFFFFu;
+    sl_raw[j] = 0;
+    sl_start[j] = 0xFFFFFFFFu;
     const uint32_t li = (uint32_t)(pk >> (48 + 8 * j)) & 0xFFu;
-    if (HASH && li != 0xFFu) sl[j] = spec[(uint64_t)blockIdx.x * kListCap + li];
+    if (HASH && li != 0xFFu) {
+      sl_raw[j] = spec_raw[(uint64_t)blockIdx.x * kListCap + li];
+      sl_start[j] = spec_start[(uint64_t)blockIdx.x * kListCap + li];
+    }
   }
   // a span with more than kEvCap events (rare): its candidate masks from the file, each
   // candidate's byte read back (no LDS, so the kernel keeps its occupancy)
@@ -685,7 +769,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
   for_events([&](uint32_t o, uint32_t t) { acc.add(t, rel + o + 1); });
   LFn pre;
   Scan(tmp).ExclusiveScan(live ? acc.fn() : lfn_id(), pre, lfn_id(), LCompose());
-  TState s = gapply(gfn_of(pre, base), gapply(ein, TState{0, 0, 0, 0}));
+  TState s = gapply(gfn_of(pre, base), gapply(ein, tin));
   const uint64_t lim = min(count[0], cap);
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
   uint32_t j = 0;           // cut events of this span so far
@@ -710,9 +794,9 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
       uint64_t raw = 0;
 #pragma unroll
       for (uint32_t q = 0; q < kSlots; ++q)
-        if (j == q && sl[q].start == want) {
+        if (j == q && sl_start[q] == want) {
           hit = true;
-          raw = sl[q].raw;
+          raw = sl_raw[q];
         }
       if (hit) {
         a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
@@ -808,18 +892,22 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
 // per-device lock for the call) while it stays within kScratchKeep: per-call pool
 // allocations of this size cost ~0.15 ms per hipFreeAsync on MI355X (rocprofv3
 // --runtime-trace, profiles/r03f_import_api_stats.csv), more than the scan itself.
+// The entry-state scan's counter lives in a second buffer that is never freed: it must be
+// zero at every call (the scan leaves it zero), so it is cleared only when allocated.
 struct TsvScratch {
   std::mutex mu;
   void* p = nullptr;
   size_t bytes = 0;
+  void* cnt = nullptr;  // done (u32) at 0, count (u64) at 8
 };
 TsvScratch g_tsv[64];
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// TSV: pass A, the scan of block functions, the count, pass B (when recs), one read-back.
-// Temporaries per 16 KiB block: its function (2 x 48 B), 8 B of events per 128 B span,
-// and the block's list of speculative key states (16 B each, up to kListCap).
+// TSV: pass A, the scan of block functions (and the count), pass B (when recs), one
+// read-back.  Temporaries per 16 KiB block: its function and in-tile prefix (2 x 48 B),
+// 8 B of events per 128 B span, and the block's list of speculative key states (10 B
+// each, up to kListCap); per tile of kTile blocks its function and entry state.
 static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
                       hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
   const uint64_t nblk = (size + kTChunk - 1) / kTChunk;
@@ -834,12 +922,11 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
     *herr = e;
     return K2H_AMD_EHIP;
   }
-  size_t tmp_bytes = 0;
-  tr(hipcub::DeviceScan::ExclusiveScan(nullptr, tmp_bytes, (GFn*)nullptr, (GFn*)nullptr, GCompose(), gfn_id(), nblk,
-                                       stream));
-  const size_t o_fn = 0, o_excl = o_fn + align256(nblk * sizeof(GFn)), o_cnt = o_excl + align256(nblk * sizeof(GFn));
-  const size_t o_ev = o_cnt + 256, o_spec = o_ev + align256(nblk * kTThreads * 8);
-  const size_t o_tmp = o_spec + align256(nblk * kListCap * sizeof(SpecSlot)), total = o_tmp + align256(tmp_bytes + 1);
+  const uint64_t ntile = (nblk + kTile - 1) / kTile;
+  const size_t o_fn = 0, o_in = o_fn + align256(nblk * sizeof(GFn)), o_tf = o_in + align256(nblk * sizeof(GFn));
+  const size_t o_ti = o_tf + align256(ntile * sizeof(GFn)), o_ev = o_ti + align256(ntile * sizeof(TState));
+  const size_t o_spec = o_ev + align256(nblk * kTThreads * 8), o_start = o_spec + align256(nblk * kListCap * 8);
+  const size_t total = o_start + align256(nblk * kListCap * 2);
   TsvScratch& sc = g_tsv[dev];
   std::lock_guard<std::mutex> lk(sc.mu);
   if (e == hipSuccess && sc.bytes < total) {
@@ -849,31 +936,43 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
     tr(hipMalloc(&sc.p, total));
     if (e == hipSuccess) sc.bytes = total;
   }
+  if (e == hipSuccess && !sc.cnt) {
+    tr(hipMalloc(&sc.cnt, 256));
+    tr(hipMemsetAsync(sc.cnt, 0, 256, stream));
+    if (e != hipSuccess) sc.cnt = nullptr;
+  }
   uint8_t* base = (uint8_t*)sc.p;
-  GFn* fn = (GFn*)(base + o_fn);
-  GFn* excl = (GFn*)(base + o_excl);
-  uint64_t* dcount = (uint64_t*)(base + o_cnt);
+  uint8_t* cb = (uint8_t*)sc.cnt;
+  EntryScan es;
+  es.blk_fn = (GFn*)(base + o_fn);
+  es.intile = (GFn*)(base + o_in);
+  es.tile_fn = (GFn*)(base + o_tf);
+  es.tile_in = (TState*)(base + o_ti);
+  es.done = (uint32_t*)cb;
+  es.count = (uint64_t*)(cb + 8);
+  es.nblk = nblk;
+  es.ntile = ntile;
+  uint64_t* dcount = es.count;
   uint64_t* ev = (uint64_t*)(base + o_ev);
-  SpecSlot* spec = (SpecSlot*)(base + o_spec);
-  void* tmp = base + o_tmp;
+  const SpecList spec{(uint64_t*)(base + o_spec), (uint16_t*)(base + o_start)};
   const bool walk = recs && cap;
   const SpadTable sp = make_spad(seed);
   if (e == hipSuccess) {
-    tsv_a_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, fn, ev, spec, sp);
+    tsv_a_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, es.blk_fn, ev, spec, sp);
     e = hipGetLastError();
   }
-  tr(hipcub::DeviceScan::ExclusiveScan(tmp, tmp_bytes, fn, excl, GCompose(), gfn_id(), nblk, stream));
   if (e == hipSuccess) {
-    tsv_count_kernel<<<1, 1, 0, stream>>>(excl, fn, nblk, dcount);
+    tsv_scan_kernel<<<(unsigned)ntile, kTThreads, 0, stream>>>(es);
     e = hipGetLastError();
   }
   if (e == hipSuccess && walk) {
     if (h1)
-      tsv_b_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, ev, spec, dcount, cap, recs, sp, h1,
-                                                                   h2);
+      tsv_b_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, es.intile, es.tile_in, ev, spec.raw,
+                                                                   spec.start, dcount, cap, recs, sp, h1, h2);
     else
-      tsv_b_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, excl, ev, spec, dcount, cap, recs, sp,
-                                                                    nullptr, nullptr);
+      tsv_b_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, es.intile, es.tile_in, ev, spec.raw,
+                                                                    spec.start, dcount, cap, recs, sp, nullptr,
+                                                                    nullptr);
     e = hipGetLastError();
   }
   uint64_t n = 0;

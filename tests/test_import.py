@@ -146,7 +146,8 @@ def test_device_scan_fuzz(cuda, fmt):
     NULs, every EOF shape), sizes across the 64-byte thread span and 16 KiB block
     boundaries, and unaligned device bases: device scan == host scan."""
     rng = np.random.default_rng(0x6B32 + (fmt == "mdbm"))
-    sizes = list(range(0, 80)) + [127, 128, 129, 16383, 16384, 16385, 40000, 200001]
+    # (8 MiB + 40001: two tiles of the TSV entry-state scan, the second one partial)
+    sizes = list(range(0, 80)) + [127, 128, 129, 16383, 16384, 16385, 40000, 200001, (8 << 20) + 40001]
     for k, size in enumerate(sizes):
         data = _fuzz_file(rng, size, fmt)
         shift = k % 5

@@ -6,6 +6,8 @@ product launch, each result digest-checked against the reference first.
       config 5 (1M x 4 KiB): variant:waves_per_cu
   python tools/lab_ab.py csr --variants 0 1 2
       config 3 (64M CSR keys)
+  python tools/lab_ab.py ralle --variants 0 1
+      bench's RALLEDATA workload (8M records)
 
 Prints one JSON object (per-variant median / min launch time in microseconds)."""
 from __future__ import annotations
@@ -33,12 +35,15 @@ def lab_lib():
     if hasattr(lib, "k2h_lab_csr"):
         lib.k2h_lab_csr.restype = ctypes.c_int
         lib.k2h_lab_csr.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+    if hasattr(lib, "k2h_lab_ralle"):
+        lib.k2h_lab_ralle.restype = ctypes.c_int
+        lib.k2h_lab_ralle.argtypes = [ctypes.c_int, _p, _p, _p, _p, _u64, _p, _p, _p]
     return lib
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("config", choices=["lines", "csr"])
+    ap.add_argument("config", choices=["lines", "csr", "ralle"])
     ap.add_argument("--variants", nargs="+", required=True)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
@@ -67,6 +72,29 @@ def main():
             rc = lib.k2h_lab_lines(var, ctypes.c_void_p(keys.data_ptr()), L, n, ctypes.c_void_p(h1.data_ptr()),
                                    None, wpc, sh)
             assert rc == 0, rc
+    elif args.config == "ralle":
+        _, n, ((klo, khi), (vlo, vhi)), _ = bench.CONFIGS["ralledata"]
+        ko = batch.synth_offsets(n, dev, klo, khi)
+        vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7)
+        kb, vb = int(ko[-1].item()), int(vo[-1].item())
+        kd = batch.synth_bytes(kb, dev)
+        vd = batch.synth_bytes(vb, dev, byte_off=1 << 33)
+        total = 80 * n + kb + vb
+        blob = torch.zeros((total + 7) // 8 * 8, dtype=torch.uint8, device=dev)
+        boff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        g = json.loads((ROOT / "tests" / "golden" / "ralledata_digest.json").read_text())
+        h1 = None
+
+        def launch(v):
+            rc = lib.k2h_lab_ralle(int(v), ctypes.c_void_p(kd.data_ptr()), ctypes.c_void_p(ko.data_ptr()),
+                                   ctypes.c_void_p(vd.data_ptr()), ctypes.c_void_p(vo.data_ptr()), n,
+                                   ctypes.c_void_p(blob.data_ptr()), ctypes.c_void_p(boff.data_ptr()), sh)
+            assert rc == 0, rc
+
+        def verify():
+            ok = g["n"] == n and g["bytes"] == total and bench.digest_dev(blob.view(torch.int64), 0) == g["blob"] \
+                and bench.digest_dev(boff, 0) == g["blob_off"]
+            return {"ok": ok}
     else:
         n = 1 << 26
         off = batch.synth_offsets(n, dev, 8, 256)
@@ -81,6 +109,13 @@ def main():
 
     res = {}
     for v in args.variants:  # parity first
+        if args.config == "ralle":
+            blob.zero_()
+            boff.zero_()
+            launch(v)
+            torch.cuda.synchronize()
+            res[v] = {"verify": verify()}
+            continue
         h1.zero_()
         launch(v)
         torch.cuda.synchronize()

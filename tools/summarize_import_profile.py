@@ -1,6 +1,7 @@
 """Summarise tools/gpu/r02ar.sh (rocprofv3 over tools/import_step.py): per call of
 k2h_amd_import_scan_prehash_device, the kernel time and the PMC counters summed over its
-kernels (tsv_a, the block-function scan, tsv_count, tsv_b), averaged over the last
+kernels (tsv_a, tsv_b; round-3 trees before r03i also the block-function scan and
+tsv_count), averaged over the last
 calls -> profiles/traffic_import.json, profiles/valu_import.json (bench.py's
 secondary.import roofline) and profiles/<tag>_import_summary.json.
 
@@ -15,7 +16,7 @@ import sys
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parents[1]
-OURS = ("tsv_a_kernel", "tsv_count_kernel", "tsv_b_kernel", "ROCPRIM_400200")  # rocprim 4.2: our scan
+OURS = ("tsv_a_kernel", "tsv_count_kernel", "tsv_b_kernel", "tsv_scan_kernel", "ROCPRIM_400200")  # rocprim 4.2: our scan
 
 
 def ours(name):
@@ -33,7 +34,7 @@ def main():
     per = collections.defaultdict(float)
     for r in rows[first:]:
         nm = r["Kernel_Name"]
-        key = next((k for k in OURS[:3] if k in nm), "lookback_scan" if "lookback" in nm else "rocprim_scan")
+        key = next((k for k in OURS[:4] if k in nm), "lookback_scan" if "lookback" in nm else "rocprim_scan")
         per[key] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / calls
     gpu_us = sum(per.values()) / 1e3
     shutil.copy(src / "trace" / "run_kernel_stats.csv", prof / f"{tag}_import_kernel_stats.csv")
@@ -51,7 +52,7 @@ def main():
         for k, v in acc.items():
             pmc[k] = v / ncalls
     traffic = int(2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024)
-    kern = "tsv_a_kernel + block-function scan + tsv_count_kernel + tsv_b_kernel<true> (one call)"
+    kern = " + ".join(sorted(per)) + " (one call)"
     (prof / "traffic_import.json").write_text(json.dumps({
         "kernel": kern, "hbm_bytes_per_launch": traffic, "FETCH_SIZE_kB": pmc["FETCH_SIZE"],
         "WRITE_SIZE_kB": pmc["WRITE_SIZE"], "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
@@ -61,7 +62,7 @@ def main():
         "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"), "round": tag, "keys_per_launch": 1 << 23}, indent=1) + "\n")
     s = {"per_kernel_us_per_call": {k: v / 1e3 for k, v in per.items()}, "gpu_us_per_call": gpu_us,
          "pmc_per_call": pmc, "hbm_bytes_per_call": traffic,
-         "source": "tools/gpu/r02ar.sh: rocprofv3 over tools/import_step.py (8M-record TSV, 1.16 GB)"}
+         "source": "tools/gpu/r03_import_prof.sh: rocprofv3 over tools/import_step.py (8M-record TSV, 1.16 GB)"}
     (prof / f"{tag}_import_summary.json").write_text(json.dumps(s, indent=1) + "\n")
     print(json.dumps(s, indent=1))
 
