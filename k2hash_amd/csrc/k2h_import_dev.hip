@@ -292,26 +292,26 @@ constexpr uint32_t kTThreads = 128;
 constexpr uint32_t kTBytes = 128;                               // bytes per thread
 constexpr uint32_t kTChunk = kTThreads * kTBytes;               // 16 KiB per block
 
-// Block-local function of a span; positions are block-relative + 1 (0: none).
-//   a: bit 0 / 1 = exit mode entering K / V (1 = V); bits [2, 17) / [17, 32) = record ends
-//      passed entering K / V;  b: last boundary entering K (low half) / V (high half);
-//   c: last NUL.
+// Block-local function of a span; positions are block-relative + 1 (0: none).  Every
+// field is a pair of 16-bit halves, low = entering in K, high = entering in V:
+//   sel:  the exit mode, as a v_perm byte selector (0x0100 = K, 0x0302 = V), so that
+//         "take y's half for x's exit mode" is one v_perm_b32 with x.sel -- for y's modes,
+//         record ends and boundaries alike (round 3: ~30 ops per compose -> 6);
+//   cnt:  record ends passed;  last: last field boundary;  c: last NUL (one 32-bit value).
 struct LFn {
-  uint32_t a, b, c;
+  uint32_t sel, cnt, last, c;
 };
-__device__ inline LFn lfn_id() { return LFn{2u, 0u, 0u}; }
+constexpr uint32_t kSelK = 0x0100u, kSelV = 0x0302u;
+__device__ inline LFn lfn_id() { return LFn{kSelK | (kSelV << 16), 0u, 0u, 0u}; }
+__device__ inline uint32_t lfn_mode(uint32_t sel, uint32_t entry) { return (sel >> (16 * entry + 1)) & 1u; }
 struct LCompose {  // x, then y
   __device__ LFn operator()(const LFn& x, const LFn& y) const {
-    const uint32_t mk = x.a & 1u, mv = (x.a >> 1) & 1u;  // mode after x, entered in K / V
-    const uint32_t yc0 = (y.a >> 2) & 0x7FFFu, yc1 = y.a >> 17;
-    const uint32_t ck = ((x.a >> 2) & 0x7FFFu) + (mk ? yc1 : yc0), cv = (x.a >> 17) + (mv ? yc1 : yc0);
-    const uint32_t yl0 = y.b & 0xFFFFu, yl1 = y.b >> 16;
-    const uint32_t lk = max(x.b & 0xFFFFu, mk ? yl1 : yl0), lv = max(x.b >> 16, mv ? yl1 : yl0);
-    LFn r;
-    r.a = ((y.a >> mk) & 1u) | (((y.a >> mv) & 1u) << 1) | (ck << 2) | (cv << 17);
-    r.b = lk | (lv << 16);
-    r.c = max(x.c, y.c);
-    return r;
+    typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+    const uint32_t yc = __builtin_amdgcn_perm(y.cnt, y.cnt, x.sel), yl = __builtin_amdgcn_perm(y.last, y.last, x.sel);
+    const u16x2 cnt = __builtin_bit_cast(u16x2, x.cnt) + __builtin_bit_cast(u16x2, yc);
+    const u16x2 last = __builtin_elementwise_max(__builtin_bit_cast(u16x2, x.last), __builtin_bit_cast(u16x2, yl));
+    return LFn{__builtin_amdgcn_perm(y.sel, y.sel, x.sel), __builtin_bit_cast(uint32_t, cnt),
+               __builtin_bit_cast(uint32_t, last), max(x.c, y.c)};
   }
 };
 
@@ -338,12 +338,12 @@ struct GCompose {
 };
 __device__ inline GFn gfn_of(const LFn& l, uint64_t base) {
   GFn g;
-  g.map = l.a & 3u;
+  g.map = lfn_mode(l.sel, 0) | (lfn_mode(l.sel, 1) << 1);
   g.pad = 0;
-  g.cnt0 = (l.a >> 2) & 0x7FFFu;
-  g.cnt1 = l.a >> 17;
-  g.last0 = (l.b & 0xFFFFu) ? base + (l.b & 0xFFFFu) : 0;
-  g.last1 = (l.b >> 16) ? base + (l.b >> 16) : 0;
+  g.cnt0 = l.cnt & 0xFFFFu;
+  g.cnt1 = l.cnt >> 16;
+  g.last0 = (l.last & 0xFFFFu) ? base + (l.last & 0xFFFFu) : 0;
+  g.last1 = (l.last >> 16) ? base + (l.last >> 16) : 0;
   g.lnul = l.c ? base + l.c : 0;
   return g;
 }
@@ -435,27 +435,24 @@ constexpr uint32_t kEvCap = 5;
 constexpr uint64_t kNoSlots = 0xFFFFull << 48;
 constexpr uint64_t kEvOverflow = (7ull << 45) | kNoSlots;
 __device__ inline uint32_t ev_count(uint64_t pk) { return (uint32_t)(pk >> 45) & 7u; }
-__device__ inline uint32_t ev_type(uint32_t c) { return c == 0x0Au ? 1u : c == 0x09u ? 2u : c == 0u ? 3u : 0u; }
+// 0x0A -> 1, 0x09 -> 2, 0x00 -> 3, other bytes 0: two bits per byte value below 11
+__device__ inline uint32_t ev_type(uint32_t c) { return c < 11u ? (0x180003u >> (2 * c)) & 3u : 0u; }
 
-// The span function (positions + 1) of an event sequence: per entry mode the exit mode, the
-// record ends passed and the last boundary; the last NUL.
-struct FnAcc {
-  uint32_t s0 = 0, s1 = 1, c0 = 0, c1 = 0, l0 = 0, l1 = 0, ln = 0;
-  __device__ void add(uint32_t type, uint32_t p1) {
-    if (type == 1u) {
-      if (s0) ++c0, l0 = p1, s0 = 0;
-      if (s1) ++c1, l1 = p1, s1 = 0;
-    } else if (type == 2u) {
-      if (!s0) l0 = p1, s0 = 1;
-      if (!s1) l1 = p1, s1 = 1;
-    } else if (type == 3u) {
-      ln = p1;
-    }
-  }
-  __device__ LFn fn() const { return LFn{s0 | (s1 << 1) | (c0 << 2) | (c1 << 17), l0 | (l1 << 16), ln}; }
-};
+// The function of one event at position p1 (block-relative + 1), composed onto a span's
+// accumulated function without branches (round 3; the per-type branches cost ~50 SALU and
+// ~45 VALU instructions per event):
+//   newline: entered in K, part of the key (exit K); entered in V, the record ends (exit K,
+//            one record end, boundary p1);
+//   TAB:     entered in K, the key ends (exit V, boundary p1); entered in V, part of the value;
+//   NUL:     the last NUL; any other byte (type 0): the identity.
+__device__ inline LFn ev_fn(uint32_t t, uint32_t p1) {
+  const bool nl = t == 1u, tab = t == 2u;
+  return LFn{nl ? (kSelK | (kSelK << 16)) : tab ? (kSelV | (kSelV << 16)) : (kSelK | (kSelV << 16)),
+             nl ? 0x10000u : 0u, nl ? p1 << 16 : tab ? p1 : 0u, t == 3u ? p1 : 0u};
+}
 
-// Walk the events of a span staged at `span` (its candidate masks), calling f(offset, type).
+// Walk the candidate bytes of a span staged at `span`, calling f(offset, type) for each
+// (type 0 for a candidate that is no event: f must treat it as none).
 template <class F>
 __device__ inline void span_events(const uint8_t* span, F&& f) {
   uint64_t mm[2];
@@ -463,8 +460,7 @@ __device__ inline void span_events(const uint8_t* span, F&& f) {
   uint32_t o = next_event(mm[0], mm[1]), c = span[o & 127u];
   while (o < 128) {
     const uint32_t on = next_event(mm[0], mm[1]), cn = span[on & 127u];
-    const uint32_t t = ev_type(c);
-    if (t) f(o, t);
+    f(o, ev_type(c));
     o = on;
     c = cn;
   }
@@ -519,13 +515,29 @@ __device__ inline NlSum nl_compose(NlSum x, NlSum y) {
   if (y.v & 1u) return y;
   return NlSum{x.v & ((y.v & 2u) ? ~0u : ~2u)};  // y has no newline; its bit 1 = "no cut in y"
 }
-struct ScanA {
-  LFn fn;
-  NlSum nl;
+struct NlOp {
+  __device__ uint32_t operator()(uint32_t x, uint32_t y) const { return nl_compose(NlSum{x}, NlSum{y}).v; }
 };
-struct ScanAOp {
-  __device__ ScanA operator()(const ScanA& x, const ScanA& y) const { return ScanA{LCompose()(x.fn, y.fn), nl_compose(x.nl, y.nl)}; }
-};
+
+// The block's function: pass A needs only the reduction of its span functions (pass B
+// rebuilds the per-span prefixes), so an order-preserving shuffle-down tree per wave and
+// the two wave results composed in order -- about half a block scan's instructions.
+__device__ inline LFn block_fn_reduce(LFn r, LFn* s_wave) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (uint32_t off = 1; off < 64; off <<= 1) {
+    const LFn y{(uint32_t)__shfl_down((int)r.sel, off, 64), (uint32_t)__shfl_down((int)r.cnt, off, 64),
+                (uint32_t)__shfl_down((int)r.last, off, 64), (uint32_t)__shfl_down((int)r.c, off, 64)};
+    const LFn c = LCompose()(r, y);
+    if (lane + off < 64) r = c;
+  }
+  if (lane == 0) s_wave[threadIdx.x >> 6] = r;
+  __syncthreads();
+  LFn t = s_wave[0];
+#pragma unroll
+  for (uint32_t w = 1; w < kTThreads / 64; ++w) t = LCompose()(t, s_wave[w]);
+  return t;
+}
 
 // Entry states of the blocks (tsv_scan_kernel, one launch instead of a device scan and a
 // count kernel): blocks form tiles of kTile, each tile scanned by one block into each
@@ -589,35 +601,36 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
   __shared__ uint64_t s_key[kListCap];  // emitted keys: start | len << 16 | slot index << 32
   __shared__ uint32_t s_nk;
-  typedef hipcub::BlockScan<ScanA, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> Scan;
-  __shared__ typename Scan::TempStorage tmp;
+  typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
+  __shared__ typename NlScan::TempStorage tmp;
+  __shared__ LFn s_wave[kTThreads / 64];
   if (threadIdx.x == 0) s_nk = 0;
   tsv_stage(f, size, blockIdx.x, lds);  // (its barrier publishes s_nk = 0)
   const uint32_t rel = kTBytes * threadIdx.x;
   const uint8_t* span = lds + 16 + rel;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
   const bool live = base + rel < size;
-  FnAcc acc;
+  LFn acc = lfn_id();
   uint64_t pk = 0;
   uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
   if (live)
-    span_events(span, [&](uint32_t o, uint32_t t) {
-      acc.add(t, rel + o + 1);
-      if (ne < kEvCap) pk |= (uint64_t)(o | (t << 7)) << (9 * ne);
-      ++ne;
-      if (t == 1u) nl = 1u | 2u | ((rel + o) << 2);
-      else nl &= ~2u;
+    span_events(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
+      acc = LCompose()(acc, ev_fn(t, rel + o + 1));
+      const uint64_t e = (uint64_t)(o | (t << 7)) << (9 * min(ne, kEvCap - 1));
+      pk |= (t && ne < kEvCap) ? e : 0ull;
+      ne += t ? 1u : 0u;
+      nl = t == 1u ? (1u | 2u | ((rel + o) << 2)) : t ? (nl & ~2u) : nl;
     });
   const bool over = ne > kEvCap;
   pk = over ? kEvOverflow : pk | ((uint64_t)ne << 45) | kNoSlots;
-  ScanA pre, agg;
-  Scan(tmp).ExclusiveScan(ScanA{live ? acc.fn() : lfn_id(), NlSum{live ? nl : 2u}}, pre,
-                          ScanA{lfn_id(), NlSum{2u}}, ScanAOp(), agg);
-  if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(agg.fn, base);
+  uint32_t pre_nl;
+  NlScan(tmp).ExclusiveScan(live ? nl : 2u, pre_nl, 2u, NlOp());
+  const LFn bf = block_fn_reduce(acc, s_wave);
+  if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(bf, base);
   // keys ending at this span's cuts: the newline state entering the span, then its events;
   // each key goes to the block's list, hashed below one lane per key
-  bool open = (pre.nl.v & 3u) == 3u;
-  uint32_t start = (pre.nl.v >> 2) + 1, j = 0;
+  bool open = (pre_nl & 3u) == 3u;
+  uint32_t start = (pre_nl >> 2) + 1, j = 0;
   if (live && !over) {
     for (uint32_t q = 0; q < ne; ++q) {
       const uint32_t e = (uint32_t)(pk >> (9 * q)) & 0x1FFu;
@@ -695,7 +708,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
                                                           const uint64_t* __restrict__ count, uint64_t cap,
                                                           k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
                                                           uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
-  typedef hipcub::BlockScan<LFn, kTThreads> Scan;
+  typedef hipcub::BlockScan<LFn, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> Scan;
   __shared__ typename Scan::TempStorage tmp;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
   const uint32_t rel = kTBytes * threadIdx.x;
@@ -765,10 +778,10 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
       }
     }
   };
-  FnAcc acc;
-  for_events([&](uint32_t o, uint32_t t) { acc.add(t, rel + o + 1); });
+  LFn acc = lfn_id();
+  for_events([&](uint32_t o, uint32_t t) { acc = LCompose()(acc, ev_fn(t, rel + o + 1)); });
   LFn pre;
-  Scan(tmp).ExclusiveScan(live ? acc.fn() : lfn_id(), pre, lfn_id(), LCompose());
+  Scan(tmp).ExclusiveScan(acc, pre, lfn_id(), LCompose());
   TState s = gapply(gfn_of(pre, base), gapply(ein, tin));
   const uint64_t lim = min(count[0], cap);
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
