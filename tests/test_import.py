@@ -256,3 +256,33 @@ def test_bench_import_workload_digest(cuda):
             "h2": h2}
     for k, v in cols.items():
         assert bench.digest_dev(v.contiguous(), 0) == g[k], k
+
+
+@pytest.mark.gpu
+def test_device_scan_over_4gib_tile_scan_runs(cuda):
+    """A TSV file above 4 GiB (bench's 1.16 GB workload four times over: 282,643 blocks of
+    16 KiB, 553 tiles): the tile-level entry-state scan runs its long-run form (more than
+    four tiles per thread) and the grow-only scratch exceeds its keep size.  Each copy's
+    records equal the single file's, offset by the copy's position; the hashes repeat."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, str(GOLDEN.parents[1]))
+    import bench
+
+    one = bench.import_workload(cuda)
+    size = one.numel()
+    r1, a1, b1 = archive.import_scan_prehash_device(one)
+    four = one.repeat(4)
+    del one
+    r4, a4, b4 = archive.import_scan_prehash_device(four)
+    torch.cuda.synchronize()
+    n = r1.shape[0]
+    assert four.numel() > 4 << 30 and (four.numel() + (16 << 10) - 1) // (16 << 10) > 4 * 512 * 128
+    assert r4.shape[0] == 4 * n
+    for c in range(4):
+        part = r4[c * n:(c + 1) * n]
+        assert torch.equal(part[:, 0] - c * size, r1[:, 0]) and torch.equal(part[:, 2] - c * size, r1[:, 2]), c
+        assert torch.equal(part[:, 1], r1[:, 1]) and torch.equal(part[:, 3], r1[:, 3]), c
+        assert torch.equal(a4[c * n:(c + 1) * n], a1) and torch.equal(b4[c * n:(c + 1) * n], b1), c
