@@ -79,6 +79,10 @@ def parse(argv=None):
     p.add_argument("--no-secondary", action="store_true", help="N=1: skip the secondary configs")
     p.add_argument("--no-verify", action="store_true", help="skip the digest checks")
     p.add_argument("--backend", default="nccl", help="torch.distributed backend for N>1 (nccl = RCCL)")
+    p.add_argument("--dist", action="store_true",
+                   help="initialise torch.distributed even at world size 1 (under torchrun): rehearses the "
+                        "N>1 path -- RCCL init with device_id and timeout, barriers, the MAX all-reduce, "
+                        "the gather -- on one GPU")
     p.add_argument("--rehearse-cpu", action="store_true",
                    help="no GPU: run the launcher / shard / gather path on CPU with the scalar plugin "
                         "(a rehearsal of the N>1 plumbing, not a measurement)")
@@ -367,7 +371,8 @@ def timed(step, steps: int, warmup: int, warm_ms: float, world: int = 1, dist=No
         extra += 10
         torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
+    distributed = dist is not None and dist.is_initialized()  # (N > 1, or --dist at N = 1)
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -377,10 +382,10 @@ def timed(step, steps: int, warmup: int, warm_ms: float, world: int = 1, dist=No
     e1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = t1 - t0
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -764,7 +769,8 @@ def main():
     ndev = torch.cuda.device_count()
     dev = torch.device("cuda", local % max(ndev, 1))  # one process per GPU; wraps only in rehearsals
     torch.cuda.set_device(dev)
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
         import datetime
 
         tmo = datetime.timedelta(seconds=args.init_timeout)
@@ -852,14 +858,14 @@ def main():
             verify = {"ok": rank != 0 or digest_dev(outs[0][0], 0) == g["h1"], "chunks_checked": 1}
         else:
             verify = verify_chunks(outs[0][0], first, g.get("chunks") or [dict(first=0, count=g["n"], h1=g["h1"])])
-        if world > 1:
+        if use_dist:
             t = torch.tensor([0 if verify["ok"] else 1, verify["chunks_checked"]], dtype=torch.int64, device=dev)
             dist.all_reduce(t)
             verify = {"ok": int(t[0].item()) == 0, "chunks_checked": int(t[1].item()), "ranks": world}
 
     # --- config 4: the RCCL gather of every shard's hashes to rank 0 ------------------------
     gather = None
-    if world > 1:
+    if use_dist:
         counts = shard.shard_counts(KEYS_1G, world) if strong and not args.keys else [n] * world
         h = outs[0][0]
         gsteps = max(3, min(10, args.steps // 10))
@@ -961,7 +967,7 @@ def main():
         if secondary:
             line["secondary"] = secondary
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

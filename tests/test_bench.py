@@ -96,6 +96,31 @@ def test_bench_two_ranks_one_gpu():
 
 
 @pytest.mark.gpu
+def test_bench_rccl_path_one_rank():
+    """The driver's N>1 command form (torch.distributed.run, one process per GPU) at one
+    rank with --dist: RCCL (backend nccl) initialised with device_id and a timeout, the
+    barrier-bracketed timing with its MAX all-reduce on a device tensor, and the gather, on
+    the one GPU this box has (two ranks cannot share a GPU under RCCL).  The 8-GPU run
+    itself is the driver's."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"),
+                        "--gpus", "1", "--dist", "--config", "fixed32_1g", "--keys", "262144", "--steps", "5",
+                        "--warmup", "1", "--warm-ms", "5"], capture_output=True, text=True, timeout=600, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 1 and line["scaling"] == "strong"
+    assert line["gather"]["backend"] == "nccl" and line["gather"]["with_gather"]["value"] > 0
+
+
+@pytest.mark.gpu
 def test_bench_n1_headline_verified():
     line = _run(["--steps", "5", "--warmup", "2", "--warm-ms", "10", "--no-secondary", "--no-cpu-baseline"], 600)
     assert line["n_gpus"] == 1 and line["verify"]["ok"] is True
