@@ -450,7 +450,21 @@ __global__ __launch_bounds__(256) void fnv_csr_staged_kernel(const uint8_t* __re
     }
     s_mask[tid] = make_uint4(w[0], w[1], w[2], w[3]);
   }
-  for (uint32_t k = tid; k <= cnt; k += NT) s_rel[k] = (uint32_t)(offsets[t0 + k] - o0);
+  {  // a thread's three offset loads in flight together (a loop waited for each in turn:
+     // round-3 lab A/B, -2 % on config 3, profiles/r03r_csr_ab.json)
+    uint32_t r[3];
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) {
+      const uint32_t k = tid + NT * q;
+      r[q] = k <= cnt ? (uint32_t)offsets[t0 + k] : 0u;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 3; ++q) {
+      const uint32_t k = tid + NT * q;
+      if (k <= cnt) s_rel[k] = r[q] - (uint32_t)o0;
+    }
+  }
+  static_assert(3 * NT >= TK + 1, "three offsets per thread cover the tile");
   __syncthreads();
 
   // DMA of the tile span (16-byte pieces; pieces past the span re-read its last piece

@@ -3,4 +3,5 @@
 #include "k2h_csr.hip"
 
 #include "lab_lines.inc"
+#include "lab_csr_setup.inc"
 #include "lab_csr.inc"
