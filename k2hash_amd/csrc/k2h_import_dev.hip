@@ -370,8 +370,19 @@ __device__ inline void tsv_stage(const uint8_t* __restrict__ f, uint64_t size, u
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint64_t base = blk * kTChunk;
   const bool aligned = (((uintptr_t)(f + base)) & 15) == 0;
+  constexpr int Q = (int)(kTChunk / 16 / kTThreads);
+  if (aligned && base + kTChunk <= size) {  // block-uniform: every load in flight at once
+    u32x4 v[Q];                              // (a per-piece branch waited for each in turn)
 #pragma unroll
-  for (int q = 0; q < (int)(kTChunk / 16 / kTThreads); ++q) {
+    for (int q = 0; q < Q; ++q)
+      v[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(f + base + 16ull * (threadIdx.x + kTThreads * q)));
+#pragma unroll
+    for (int q = 0; q < Q; ++q) *reinterpret_cast<u32x4*>(lds + 16 + 16 * (threadIdx.x + kTThreads * q)) = v[q];
+    __syncthreads();
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) {
     const uint32_t piece = threadIdx.x + kTThreads * q;
     const uint64_t o = base + 16ull * piece;
     u32x4 v;

@@ -4,7 +4,8 @@
 //   2: wave 1 stages the key span itself and hashes it before the block barrier;
 //   3: the next segment's window read only for pieces that cross into it; 4: 3 with the
 //   next piece's table entry read one piece ahead; 5: the product with the table entry one
-//   piece ahead; 6: the product with the table entry and both segments one piece ahead.
+//   piece ahead; 6: the product with the table entry and both segments one piece ahead;
+//   7: the record offsets of every segment loaded without branches (one latency).
 #include "k2h_ralledata.hip"
 
 namespace k2h {
@@ -1251,6 +1252,204 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
 }
 
 
+__device__ uint64_t g_zero_pair[2] = {0, 0};  // (global, not constant: one address space with the offsets)
+// The key hashes are computed here from the staged keys (no hash kernel, no scratch).
+// Wave 0 only waits for its records' offsets (the staged loads are issued by waves 1-3).
+// 7 waves/SIMD (<= 72 VGPRs): the LDS image allows 7 blocks per CU
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void ralle_v7_kernel(
+    RalleInputs in, uint64_t n, uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off, SpadTable spad_tab) {
+  constexpr int R = kGatherRecs, NSEG = 5 * R;
+  typedef uint32_t u32x4_al __attribute__((ext_vector_type(4)));
+  __shared__ __attribute__((aligned(16))) uint8_t img[kGatherImg];
+  __shared__ int2 seg[NSEG + 1];     // segment g: .x = adj (span byte y sits at img[y + adj]), .y = its end in the span
+  __shared__ uint16_t tab[kGatherPieces];  // segment holding piece p's first byte
+  __shared__ u32x4_al qmask[17];
+  __shared__ uint64_t spad[16];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t r0 = (uint64_t)blockIdx.x * R;
+  const uint32_t nr = (uint32_t)(n - r0 < (uint64_t)R ? n - r0 : (uint64_t)R);
+  const uint64_t* offs[4] = {in.koff, in.voff, in.soff, in.aoff};
+  const uint8_t* srcs[4] = {in.keys, in.vals, in.skeys, in.attrs};
+  // the records' own offsets first: they do not depend on the span offsets below
+  // variant 7: the record offsets of all segments loaded without branches (a NULL segment
+  // reads its own lane's first offset of the key stream... or a zero word), so every load
+  // is in flight together
+  uint32_t ro0[4] = {0, 0, 0, 0}, ro1[4] = {0, 0, 0, 0};
+  if (tid < nr) {
+    uint64_t a0[4], a1[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const uint64_t* p = offs[s] ? offs[s] + r0 + tid : g_zero_pair;
+      a0[s] = p[0];
+      a1[s] = p[1];
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      ro0[s] = (uint32_t)a0[s];
+      ro1[s] = (uint32_t)a1[s];
+    }
+  }
+  // block-uniform: each input span, its aligned hull, where it goes in the image
+  uint64_t o_first = 80ull * r0, span = 80ull * nr, hull_total = 0;
+  uint64_t sbase[4], hull_lo[4], hull_n[4];
+  int32_t area[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    uint64_t b = 0, e = 0, f = 0;
+    if (offs[s]) {
+      b = offs[s][r0];
+      e = offs[s][r0 + nr];
+      f = offs[s][0];
+    }
+    sbase[s] = b;
+    o_first += b - f;
+    span += e - b;
+    const uint64_t lo = (uint64_t)(uintptr_t)(srcs[s] + b) & ~15ull, hi = ((uint64_t)(uintptr_t)(srcs[s] + e) + 15) & ~15ull;
+    hull_lo[s] = lo;
+    hull_n[s] = e > b ? (hi - lo) >> 4 : 0;
+    area[s] = kGatherHdr + 80 * R + (int32_t)(16 * hull_total) + (int32_t)((uintptr_t)(srcs[s] + b) - lo);
+    hull_total += hull_n[s];
+  }
+  if (16 * hull_total > (uint64_t)kGatherPool) {  // block-uniform: too large to stage
+    // the group form, one record per 8 lanes straight to HBM, lane 0 hashing the key
+    if (tid < 16) spad[tid] = spad_tab.v[tid];
+    __syncthreads();
+    for (uint32_t rec = tid / 8; rec < nr; rec += 32) group_record<8>(in, n, out, blob_off, r0 + rec, tid % 8, spad);
+    return;
+  }
+  // 1a. the staged pieces: up to 4 aligned loads per thread of waves 1-3 (wave 0's only
+  // loads are its records' offsets, so its record work waits for nothing else)
+  constexpr uint32_t SW = 64, NST = 256 - SW;
+  constexpr int PPT = (kGatherPool / 16 + NST - 1) / NST;
+  u32x4_al v[PPT];
+  uint32_t dst[PPT];
+#pragma unroll
+  for (int u = 0; u < PPT; ++u) {
+    const uint64_t q = (uint64_t)tid - SW + NST * u;
+    dst[u] = 0xffffffffu;
+    if (tid >= SW && q < hull_total) {
+      uint64_t addr = 0, before = 0;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        if (q >= before && q < before + hull_n[s]) addr = hull_lo[s] + 16 * (q - before);
+        before += hull_n[s];
+      }
+      v[u] = *reinterpret_cast<const u32x4_al*>((uintptr_t)addr);
+      dst[u] = kGatherHdr + 80 * R + 16 * (uint32_t)q;
+    }
+  }
+  // 1b. one thread per record: header, segment table, piece table, blob offset.  All
+  // block-relative quantities fit 32 bits once the spans fit the image.
+  const uint64_t a_out = (uint64_t)(uintptr_t)(out + o_first);
+  const int32_t d0 = (int32_t)(a_out & 15u);
+  if (tid < 17) {  // qmask[l] = bytes [l, 16) of a piece
+    u32x4_al m;
+    m.x = (uint32_t)(~0ull << (8 * min(max((int)tid - 0, 0), 4)));
+    m.y = (uint32_t)(~0ull << (8 * min(max((int)tid - 4, 0), 4)));
+    m.z = (uint32_t)(~0ull << (8 * min(max((int)tid - 8, 0), 4)));
+    m.w = (uint32_t)(~0ull << (8 * min(max((int)tid - 12, 0), 4)));
+    qmask[tid] = m;
+  }
+  if (tid < 16) spad[tid] = spad_tab.v[tid];
+  if (tid < nr) {
+    const uint64_t i = r0 + tid;
+    uint32_t rel[4], len[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      rel[s] = ro0[s] - (uint32_t)sbase[s];
+      len[s] = ro1[s] - ro0[s];
+    }
+    const int32_t B = (int32_t)(80u * tid + rel[0] + rel[1] + rel[2] + rel[3]);
+    const uint32_t kl = len[0], vl = len[1], sl = len[2], al = len[3];
+    const uint32_t f[20] = {0, 0, 0, 0, kl, 0, vl, 0, sl, 0,  // hashes: filled in by wave 0 below
+                            al, 0, 80, 0, 80 + kl, 0, 80 + kl + vl, 0, 80 + kl + vl + sl, 0};
+#pragma unroll
+    for (int c = 0; c < 5; ++c)
+      *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid + 16 * c) = u32x4_al{f[4 * c], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]};
+    int32_t start = B;
+    int32_t p = tid == 0 ? 0 : (B + d0 + 15) >> 4;  // first piece whose first byte is in this record
+#pragma unroll
+    for (int c = 0; c < 5; ++c) {
+      const uint32_t g = 5 * tid + c;
+      const int32_t L = c == 0 ? 80 : (int32_t)len[c - 1];
+      const int32_t adj = c == 0 ? kGatherHdr + 80 * (int32_t)tid - start : area[c - 1] + (int32_t)rel[c - 1] - start;
+      seg[g] = int2{adj, start + L};
+      for (; 16 * p - d0 < start + L; ++p) tab[p] = (uint16_t)g;  // pieces starting in this segment
+      start += L;
+    }
+    if (tid + 1 == nr) seg[5 * nr] = int2{kGatherHdr, start};  // read (never used) as the last segment's successor
+    if (blob_off) {
+      blob_off[i] = o_first + B;
+      if (i + 1 == n) blob_off[n] = o_first + start;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < PPT; ++u)
+    if (dst[u] != 0xffffffffu) *reinterpret_cast<u32x4_al*>(img + dst[u]) = v[u];
+  __syncthreads();
+  // 1c. wave 0 hashes the block's keys from the image into the headers
+  if (tid < nr) {
+    const uint32_t kl = ro1[0] - ro0[0], ke = ro1[0] - (uint32_t)sbase[0];
+    uint64_t h1, h2;
+    staged_key_hash(img + area[0] + ke, kl, spad, h1, h2);
+    *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid) =
+        u32x4_al{(uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32)};
+  }
+  __syncthreads();
+  // 2. aligned output pieces: the window of each segment in the piece, aligned with the
+  // piece, merged forward (segment k supplies bytes [its start, 16) over what came before)
+  const int32_t sp = (int32_t)span;
+  const uint32_t np = (uint32_t)((d0 + sp + 15) >> 4);
+  uint8_t* const base = out + (o_first - (uint64_t)d0);
+  // piece p: its first segment s0 (= seg[g]) and the next s1, both windows already read;
+  // further segments (a short or empty one between) are read here
+  auto piece = [&](uint32_t p, uint32_t g, int2 s0, int2 s1, const u32x4_ua& w0, const u32x4_ua& w1) {
+    const int32_t x = 16 * (int32_t)p - d0, end = min(x + 16, sp);
+    u32x4_al acc = {w0.x, w0.y, w0.z, w0.w};
+    int32_t pos = s0.y;
+    auto merge = [&](const u32x4_ua& w) {  // bytes [pos - x, 16) from w
+      const u32x4_al q = qmask[pos - x];
+      acc.x = (w.x & q.x) | (acc.x & ~q.x);
+      acc.y = (w.y & q.y) | (acc.y & ~q.y);
+      acc.z = (w.z & q.z) | (acc.z & ~q.z);
+      acc.w = (w.w & q.w) | (acc.w & ~q.w);
+    };
+    if (pos < end) {
+      if (s1.y > pos) {
+        merge(w1);
+        pos = s1.y;
+      }
+      ++g;
+      while (pos < end) {
+        const int2 sn = seg[++g];
+        if (sn.y > pos) {
+          merge(*reinterpret_cast<const u32x4_ua*>(img + sn.x + x));
+          pos = sn.y;
+        }
+      }
+    }
+    if (x >= 0 && x + 16 <= sp) {
+      __builtin_nontemporal_store(acc, reinterpret_cast<u32x4_al*>(base + 16ull * p));
+    } else {  // shared with a neighbouring block: this block's bytes only
+      const uint32_t wv[4] = {acc.x, acc.y, acc.z, acc.w};
+      for (int k = max(0, -x); k < 16 && x + k < sp; ++k) base[16ull * p + k] = (uint8_t)(wv[k >> 2] >> (8 * (k & 3)));
+    }
+  };
+  // A piece's next segment is read before it is known to reach into the piece (the read is
+  // then discarded), and its window can fall outside the image (e.g. a long pool segment
+  // followed by the next record's header): clamp the index into the image.
+  auto window = [&](int2 sg, uint32_t p) {
+    const int32_t at = min(max(sg.x + 16 * (int32_t)p - d0, 0), kGatherImg - 16);
+    return *reinterpret_cast<const u32x4_ua*>(img + at);
+  };
+  for (uint32_t p = tid; p < np; p += 256) {
+    const uint32_t g = tab[p];
+    const int2 s0 = seg[g], s1 = seg[g + 1];  // the piece's segment and the next, one read
+    piece(p, g, s0, s1, window(s0, p), window(s1, p));
+  }
+}
+
+
 }  // namespace
 }  // namespace k2h
 
@@ -1268,6 +1467,8 @@ extern "C" __attribute__((visibility("default"))) int k2h_lab_ralle(int variant,
   if (variant == 0) return launch_ralledata(in, n, kSeedBuiltinValue, (uint8_t*)out, (uint64_t*)blob_off, st) == hipSuccess ? 0 : 1;
   if (variant == 1)
     ralle_v1_kernel<<<g, 256, 0, st>>>(in, n, (uint8_t*)out, (uint64_t*)blob_off, make_spad(kSeedBuiltinValue));
+  else if (variant == 7)
+    ralle_v7_kernel<<<g, 256, 0, st>>>(in, n, (uint8_t*)out, (uint64_t*)blob_off, make_spad(kSeedBuiltinValue));
   else if (variant == 5)
     ralle_v5_kernel<<<g, 256, 0, st>>>(in, n, (uint8_t*)out, (uint64_t*)blob_off, make_spad(kSeedBuiltinValue));
   else if (variant == 6)
