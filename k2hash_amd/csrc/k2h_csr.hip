@@ -577,36 +577,37 @@ __global__ __launch_bounds__(256) void fnv_fixed_long_kernel(const uint8_t* __re
 
 // ---------------------------------------------------------------------------
 // Fixed-length keys of a multiple of 128 bytes from a 128-aligned base (BASELINE
-// config 5, 4 KiB): one lane per key; the keys are DMA'd into a per-wave LDS ring of D
-// rounds, round q = bytes [RB q, RB q + RB) of every lane's key (RB = 128: a whole
-// line; 64 RB bytes per round), D-1 rounds in flight while the wave hashes the current
-// one.  No VGPR transit (global_load_lds), no per-chunk address math (chunks are
-// 16-aligned, so none straddles a round), and the DMA addresses are a uniform base +
-// fixed per-lane offsets.
+// config 5, 4 KiB): one lane per key; the keys are DMA'd into a per-wave LDS ring of two
+// rounds, round q = bytes [128 q, 128 q + 128) of every lane's key (a whole line; 8 KiB
+// per round), the next round in flight while the wave hashes the current one.  No VGPR
+// transit (global_load_lds), no per-chunk address math (chunks are 16-aligned, so none
+// straddles a round).
 //
-// With NP = RB/16 pieces per round and LPI = 1024/RB lanes per DMA instruction,
-// instruction i of a round loads the pieces of lanes LPI i .. LPI i + LPI-1: lane t
-// fetches piece ((t % NP) + rot_L) % NP of lane L = LPI i + t / NP, rot_L =
-// (L / (256/RB)) % NP, into LDS byte 1024 i + 16 t.  Lane L's round then sits at
-// (L / LPI)*1024 + (L % LPI)*RB with piece j at position (j - rot_L) % NP, and when all
-// lanes read piece j together the 16 lanes of each ds_read_b128 pass hit 16 distinct
-// 4-bank groups (the row offset (L % LPI)*RB takes 256/RB bank phases, the rotation the
-// other NP).
+// Instruction i of a round loads the pieces of lanes 8i .. 8i+7: lane t fetches piece
+// ((t % 8) + rot_L) % 8 of lane L = 8i + t/8, rot_L = (L/2) % 8, into LDS byte 1024 i +
+// 16 t.  Lane L's round then sits at (L/8)*1024 + (L%8)*128 with piece j at position
+// (j - rot_L) % 8, and when all lanes read piece j together the 16 lanes of each
+// ds_read_b128 pass hit 16 distinct 4-bank groups (the row offset (L%8)*128 takes two
+// bank phases, the rotation the other eight).
+//
+// The round loop issues no VALU besides the hash (round 3; the round-2 form spent 21 per
+// round, 3 per chunk, on addresses and copies): a round's DMAs are an SGPR base + the
+// lane's fixed 32-bit offsets (line_dma8), the LDS reads fixed per-lane addresses with the
+// slot as the immediate offset (the loop unrolled over the two slots), and the state and
+// the mad64 zero half stay pinned in v48-v50 across the loop.
 //
 // Wait invariant: the only vector-memory operations a wave issues inside the round loop
-// are its DMA loads (NP per round, in order) -- no stores, no other loads -- so
-// `s_waitcnt vmcnt(NP*(D-1))` after issuing round q+D-1 means exactly "rounds <= q have
-// landed".  The hash stores come after the loop.  tests/test_kernel_source.py checks the
-// loop body for stores.
+// are its DMA loads (8 per round, in order) -- no stores, no other loads -- so
+// `s_waitcnt vmcnt(8)` after issuing round q+1 means exactly "rounds <= q have landed".
+// The hash stores come after the loop.  tests/test_kernel_source.py checks the loop body
+// for stores.
 // ---------------------------------------------------------------------------
-template <bool H2, int D, int RB, bool EPI = false>
+template <bool H2, bool EPI = false>
 __global__ __launch_bounds__(64) void fnv_fixed_lines_kernel(const uint8_t* __restrict__ base, uint64_t key_len,
                                                              uint64_t n, uint64_t seed, uint64_t* __restrict__ h1,
                                                              uint64_t* __restrict__ h2, BucketParams bp = {}) {
-  constexpr uint32_t NP = RB / 16, LPI = 1024 / RB, PH = 256 / RB;
-  static_assert((RB == 256 || RB == 128 || RB == 64) && D >= 2 && NP * (D - 1) <= 63,
-                "vmcnt holds at most 63 loads");
-  __shared__ __attribute__((aligned(1024))) uint8_t ring[D * 64 * RB];
+  constexpr uint32_t RB = 128, NP = 8, SLOT = 64 * RB;
+  __shared__ __attribute__((aligned(1024))) uint8_t ring[2 * SLOT];
   const uint32_t t = threadIdx.x;
   const uint64_t key0 = (uint64_t)blockIdx.x * 64u;
   const uint32_t last = (uint32_t)(n - key0 < 64u ? n - key0 - 1 : 63u);  // highest lane holding a key
@@ -616,48 +617,49 @@ __global__ __launch_bounds__(64) void fnv_fixed_lines_kernel(const uint8_t* __re
   uint32_t voff[NP];
 #pragma unroll
   for (uint32_t i = 0; i < NP; ++i) {
-    const uint32_t L = LPI * i + t / NP;
-    const uint32_t piece = ((t % NP) + (L / PH) % NP) % NP;
+    const uint32_t L = 8u * i + t / NP;
+    const uint32_t piece = ((t % NP) + (L / 2u) % NP) % NP;
     voff[i] = (L < last ? L : last) * kl + 16u * piece;  // lanes past the end re-read the last key
   }
-  const uint32_t rot = (t / PH) % NP;
-  const uint32_t rowb = (t / LPI) * 1024u + (t % LPI) * RB;
-  uint32_t pofs[NP];
+  const uint32_t rot = (t / 2u) % NP;
+  const uint32_t rb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)ring;
+  const uint32_t rowb = rb + (t / 8u) * 1024u + (t % 8u) * RB;
+  uint32_t a[NP];
 #pragma unroll
-  for (uint32_t j = 0; j < NP; ++j) pofs[j] = rowb + 16u * ((j + NP - rot) % NP);
-  const uint8_t* wbase = base + key0 * key_len;
-
-  auto issue = [&](uint32_t q) {
-    uint8_t* slot = ring + (q % D) * (64u * RB);
-    const uint8_t* src = wbase + (uint64_t)RB * q;
-#pragma unroll
-    for (uint32_t i = 0; i < NP; ++i)
-      __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(src + voff[i]),
-                                       (__attribute__((address_space(3))) void*)(slot + 1024u * i), 16, 0, 0);
+  for (uint32_t j = 0; j < NP; ++j) a[j] = rowb + 16u * ((j + NP - rot) % NP);
+  const uint64_t wbase = (uint64_t)(uintptr_t)(base + key0 * key_len);
+  auto issue = [&](uint32_t q, uint32_t slot) {  // round q into slot (wave-uniform source base)
+    const uint64_t s = wbase + (uint64_t)RB * q;
+    // (readfirstlane returns int: each half goes through uint32_t so the low one is not
+    // sign-extended into the high one)
+    const uint64_t src = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(s >> 32)) << 32) |
+                         (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)s);
+    line_dma8(src, rb + slot * SLOT, voff);
   };
 
-  for (uint32_t q = 0; q < D - 1 && q < R; ++q) issue(q);
-  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2 = lo, hi2 = hi;
-  for (uint32_t q = 0; q < R; ++q) {
-    // slot (q+D-1) % D held round q-1, whose reads completed inside the previous round's
-    // asm statement (lgkmcnt(0) before its last chunk)
+  uint32_t lo = (uint32_t)seed, hi = (uint32_t)(seed >> 32), lo2 = lo, hi2 = hi, z = 0;
+  issue(0, 0);
+  uint32_t q = 0;
+  for (; q + 2 < R; q += 2) {  // rounds q (slot 0) and q+1 (slot 1), neither the key's last
     asm volatile("" ::: "memory");
-    if (q + D - 1 < R) {
-      issue(q + D - 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NP * (D - 1)) : "memory");  // round q has landed (invariant above)
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    // LDS reads in asm (fnv_lds_round): the compiler's own waits would drain every DMA
-    const uint32_t sb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)(ring + (q % D) * (64u * RB));
-    uint32_t a[NP];
-#pragma unroll
-    for (uint32_t j = 0; j < NP; ++j) a[j] = sb + pofs[j];
-    if (q + 1 < R) {
-      fnv_lds_round<NP>(lo, hi, a);
-    } else {
-      fnv_lds_round_last<NP>(lo, hi, lo2, hi2, a);  // the state before the key's final byte
-    }
+    issue(q + 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // round q has landed (invariant above)
+    fnv_lds_round8o<0>(lo, hi, z, a);
+    asm volatile("" ::: "memory");  // slot 0's reads completed inside that statement
+    issue(q + 2, 0);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    fnv_lds_round8o<SLOT>(lo, hi, z, a);
+  }
+  asm volatile("" ::: "memory");
+  if (q + 1 < R) {  // two rounds left: q (slot 0), then the last, q+1 (slot 1)
+    issue(q + 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    fnv_lds_round8o<0>(lo, hi, z, a);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fnv_lds_round8o_last<SLOT>(lo, hi, z, lo2, hi2, a);  // the state before the key's final byte
+  } else {  // one round left: q, the last (slot 0)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    fnv_lds_round8o_last<0>(lo, hi, z, lo2, hi2, a);
   }
   if (t > last) return;
   const uint64_t i = key0 + t;
@@ -710,11 +712,11 @@ hipError_t launch_fixed_long(const void* keys, uint64_t key_len, uint64_t n, uin
   if (fixed_lines_ok(keys, key_len)) {  // 2 rounds of whole 128-byte lines per lane in the LDS ring
     const unsigned g = (unsigned)((n + 63) / 64);
     if (bp) {
-      if (h2) fnv_fixed_lines_kernel<true, 2, 128, true><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, h2, *bp);
-      else fnv_fixed_lines_kernel<false, 2, 128, true><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr, *bp);
+      if (h2) fnv_fixed_lines_kernel<true, true><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, h2, *bp);
+      else fnv_fixed_lines_kernel<false, true><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr, *bp);
     } else {
-      if (h2) fnv_fixed_lines_kernel<true, 2, 128><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, h2);
-      else fnv_fixed_lines_kernel<false, 2, 128><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
+      if (h2) fnv_fixed_lines_kernel<true><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, h2);
+      else fnv_fixed_lines_kernel<false><<<g, 64, 0, stream>>>(k, key_len, n, seed, h1, nullptr);
     }
     return hipGetLastError();
   }

@@ -463,4 +463,66 @@ __device__ __forceinline__ void fnv_lds_round8_last(uint32_t& lo, uint32_t& hi, 
                : K2H_R8_CLOBBERS);
 }
 
+// The same eight-chunk round with the LDS slot as the ds_read immediate offset O (the
+// per-lane addresses a[] stay fixed across rounds: no address VALU per round) and the
+// zero half of the mad64 addend pair carried in v50 by the caller (z, always 0; not
+// re-materialised per statement).
+#define K2H_R8O_BODY(LASTCHUNK)                                              \
+  "ds_read_b128 v[40:43], %[a0] offset:%[o]\n\t"                             \
+  "ds_read_b128 v[44:47], %[a1] offset:%[o]\n\t"                             \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "ds_read_b128 v[40:43], %[a2] offset:%[o]\n\t"                             \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_B                                   \
+  "ds_read_b128 v[44:47], %[a3] offset:%[o]\n\t"                             \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "ds_read_b128 v[40:43], %[a4] offset:%[o]\n\t"                             \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_B                                   \
+  "ds_read_b128 v[44:47], %[a5] offset:%[o]\n\t"                             \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "ds_read_b128 v[40:43], %[a6] offset:%[o]\n\t"                             \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_B                                   \
+  "ds_read_b128 v[44:47], %[a7] offset:%[o]\n\t"                             \
+  "s_waitcnt lgkmcnt(1)\n\t" K2H_X_CHUNK_A                                   \
+  "s_waitcnt lgkmcnt(0)\n\t" LASTCHUNK
+#define K2H_R8O_INPUTS                                                                                       \
+  [a0] "v"(a[0]), [a1] "v"(a[1]), [a2] "v"(a[2]), [a3] "v"(a[3]), [a4] "v"(a[4]), [a5] "v"(a[5]),              \
+      [a6] "v"(a[6]), [a7] "v"(a[7]), [o] "n"(O), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+
+template <int O>
+__device__ __forceinline__ void fnv_lds_round8o(uint32_t& lo, uint32_t& hi, uint32_t& z, const uint32_t (&a)[8]) {
+  asm volatile(K2H_R8O_BODY(K2H_X_CHUNK_B)
+               : "+{v48}"(lo), "+{v49}"(hi), "+{v50}"(z)
+               : K2H_R8O_INPUTS
+               : K2H_R8_CLOBBERS);
+}
+
+template <int O>
+__device__ __forceinline__ void fnv_lds_round8o_last(uint32_t& lo, uint32_t& hi, uint32_t& z, uint32_t& lo2,
+                                                     uint32_t& hi2, const uint32_t (&a)[8]) {
+  asm volatile(K2H_R8O_BODY(K2H_LAST_B)
+               : "+{v48}"(lo), "+{v49}"(hi), "+{v50}"(z), "={v60}"(lo2), "={v61}"(hi2)
+               : K2H_R8O_INPUTS
+               : K2H_R8_CLOBBERS);
+}
+
+// One round of line DMA for the line kernel: 8 global_load_lds_dwordx4, each an SGPR base
+// (`src`, wave-uniform) + the lane's 32-bit offset v[i], LDS destination m + 1024 i in M0.
+// As asm, the compiler neither counts these loads nor waits for them: every wait on them
+// is the caller's explicit s_waitcnt vmcnt.  M0 is a reserved register the compiler sets
+// before each of its own uses (it cannot be declared clobbered); the caller's kernel has
+// no other M0 user.
+#define K2H_DMA1(I, OFF)             \
+  "s_add_u32 m0, %[m], " #OFF "\n\t" \
+  "s_nop 0\n\t"                      \
+  "global_load_lds_dwordx4 %[v" #I "], %[s]\n\t"
+__device__ __forceinline__ void line_dma8(uint64_t src, uint32_t m, const uint32_t (&v)[8]) {
+  asm volatile(K2H_DMA1(0, 0) K2H_DMA1(1, 0x400) K2H_DMA1(2, 0x800) K2H_DMA1(3, 0xc00) K2H_DMA1(4, 0x1000)
+                   K2H_DMA1(5, 0x1400) K2H_DMA1(6, 0x1800) K2H_DMA1(7, 0x1c00)
+               :
+               : [s] "s"(src), [m] "s"(m), [v0] "v"(v[0]), [v1] "v"(v[1]), [v2] "v"(v[2]), [v3] "v"(v[3]),
+                 [v4] "v"(v[4]), [v5] "v"(v[5]), [v6] "v"(v[6]), [v7] "v"(v[7])
+               : "memory", "scc");
+}
+#undef K2H_DMA1
+
 }  // namespace k2h
