@@ -32,12 +32,27 @@ p.add_argument("--second", action="store_true")
 a = p.parse_args()
 
 dev = torch.device("cuda:0")
-dig = json.loads((ROOT / "tests/golden/digests.json").read_text())["configs"]
-name = {"fixed32": "fixed32_16M", "csr": "csr_8_256_64M", "fixed4096": "fixed4096_1M", "fixed21": "fixed21_1M"}[a.config]
-cfg = dig[name]
-n = cfg["n"]
+if a.config == "ralledata":  # the bench's RALLEDATA workload, checked against its oracle digest
+    import bench  # noqa: E402
+    _, n, ((klo, khi), (vlo, vhi)), _ = bench.CONFIGS["ralledata"]
+    cfg = {"kind": "ralledata"}
+    gr = json.loads((ROOT / "tests" / "golden" / "ralledata_digest.json").read_text())
+    ko = batch.synth_offsets(n, dev, klo, khi)
+    vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7)
+    kb, vb = int(ko[-1].item()), int(vo[-1].item())
+    kd = batch.synth_bytes(kb, dev)
+    vd = batch.synth_bytes(vb, dev, byte_off=1 << 33)
+    total = 80 * n + kb + vb
+    blob = torch.zeros((total + 7) // 8 * 8, dtype=torch.uint8, device=dev)
+    boff = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    algo = 2 * (kb + vb) + 104 * n  # input + blob bytes, two offset arrays in, blob offsets out
+else:
+    dig = json.loads((ROOT / "tests/golden/digests.json").read_text())["configs"]
+    name = {"fixed32": "fixed32_16M", "csr": "csr_8_256_64M", "fixed4096": "fixed4096_1M", "fixed21": "fixed21_1M"}[a.config]
+    cfg = dig[name]
+    n = cfg["n"]
 sets = []
-for s in range(2):
+for s in range(2 if cfg["kind"] != "ralledata" else 0):
     if cfg["kind"] == "fixed":
         sets.append((batch.synth_bytes(n * cfg["key_len"], dev), None))
         algo = n * cfg["key_len"] + 8 * n
@@ -59,6 +74,12 @@ for path in paths:
 
 
 def run(lib, i):
+    if cfg["kind"] == "ralledata":
+        rc = lib.k2h_amd_build_ralledata(kd.data_ptr(), ko.data_ptr(), vd.data_ptr(), vo.data_ptr(), None, None, None,
+                                         None, n, blob.data_ptr(), boff.data_ptr(), 0,
+                                         torch.cuda.current_stream().cuda_stream)
+        assert rc == 0, rc
+        return
     keys, off = sets[i & 1]
     h2 = out[1].data_ptr() if a.second else None
     stream = torch.cuda.current_stream().cuda_stream
@@ -70,6 +91,17 @@ def run(lib, i):
 
 
 for path, lib in zip(paths, libs):
+    if cfg["kind"] == "ralledata":
+        blob.zero_()
+        boff.zero_()
+        run(lib, 0)
+        torch.cuda.synchronize()
+        ok = gr["n"] == n and gr["bytes"] == total and bench.digest_dev(blob.view(torch.int64), 0) == gr["blob"] \
+            and bench.digest_dev(boff, 0) == gr["blob_off"]
+        print(f"{path}: parity {'OK' if ok else 'MISMATCH'}", flush=True)
+        if not ok:
+            sys.exit(1)
+        continue
     out[0].zero_()
     run(lib, 0)
     torch.cuda.synchronize()
