@@ -58,7 +58,9 @@ def test_fixed32_many_blocks(cuda, oracle, n):
     assert np.array_equal(host_u64(g1), r1)
 
 
-@pytest.mark.parametrize("key_len", list(range(1, 72)) + [95, 96, 97, 127, 128, 129, 255, 256, 257, 1000, 4095, 4096])
+# 384 and 640: odd round counts (3, 5) of the line-DMA kernel (two-slot unrolled loop)
+@pytest.mark.parametrize("key_len", list(range(1, 72)) + [95, 96, 97, 127, 128, 129, 255, 256, 257, 384, 640, 1000, 4095,
+                                     4096])
 def test_fixed_any_length_vs_oracle(cuda, oracle, key_len):
     import torch
     n = 517 if key_len < 1000 else 67
