@@ -162,16 +162,30 @@ __device__ __forceinline__ void staged_key_hash(const uint8_t* end, uint32_t len
 
 // The key hashes are computed here from the staged keys (no hash kernel, no scratch).
 // Wave 0 only waits for its records' offsets (the staged loads are issued by waves 1-3).
-// 7 waves/SIMD (<= 72 VGPRs): the LDS image allows 7 blocks per CU
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void ralledata_gather_kernel(
+// 8 blocks per CU (8 waves/SIMD, <= 64 VGPRs): the block's LDS stays under 20 KiB -- the
+// segment table packs (adj, end) into 16-bit halves, the piece table keeps the low byte of
+// each piece's segment index plus the full index every 64 pieces (a 64-piece run, 1 KiB,
+// meets at most 14 records -- every record carries an 80-byte header -- so fewer than 256
+// segments, and the low byte and the run's base recover the index) -- where the round-2
+// tables (int2, uint16) allowed 7 (A/B: 0.724 vs 0.733 ms, profiles/r03ad_ralle_ab.txt).
+__device__ __forceinline__ uint32_t seg_pack(int32_t adj, int32_t end) {
+  return (uint32_t)(uint16_t)(int16_t)adj | ((uint32_t)end << 16);
+}
+__device__ __forceinline__ int2 seg_unpack(uint32_t v) { return int2{(int32_t)(int16_t)(v & 0xffffu), (int32_t)(v >> 16)}; }
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void ralledata_gather_kernel(
     RalleInputs in, uint64_t n, uint8_t* __restrict__ out, uint64_t* __restrict__ blob_off, SpadTable spad_tab) {
   constexpr int R = kGatherRecs, NSEG = 5 * R;
   typedef uint32_t u32x4_al __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) uint8_t img[kGatherImg];
-  __shared__ int2 seg[NSEG + 1];     // segment g: .x = adj (span byte y sits at img[y + adj]), .y = its end in the span
-  __shared__ uint16_t tab[kGatherPieces];  // segment holding piece p's first byte
+  __shared__ uint32_t seg[NSEG + 1];  // segment g: seg_pack(adj, end): span byte y sits at img[y + adj], end in the span
+  __shared__ uint8_t tab[kGatherPieces];  // low byte of the segment holding piece p's first byte
+  __shared__ uint16_t tbase[(kGatherPieces + 63) / 64];  // segment holding piece 64 j's first byte
   __shared__ u32x4_al qmask[17];
   __shared__ uint64_t spad[16];
+  static_assert(kGatherImg + 4 * (NSEG + 1) + kGatherPieces + 2 * ((kGatherPieces + 63) / 64) + 16 * 17 + 8 * 16 <=
+                    20 * 1024,
+                "8 blocks per CU");
   const uint32_t tid = threadIdx.x;
   const uint64_t r0 = (uint64_t)blockIdx.x * R;
   const uint32_t nr = (uint32_t)(n - r0 < (uint64_t)R ? n - r0 : (uint64_t)R);
@@ -270,11 +284,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
       const uint32_t g = 5 * tid + c;
       const int32_t L = c == 0 ? 80 : (int32_t)len[c - 1];
       const int32_t adj = c == 0 ? kGatherHdr + 80 * (int32_t)tid - start : area[c - 1] + (int32_t)rel[c - 1] - start;
-      seg[g] = int2{adj, start + L};
-      for (; 16 * p - d0 < start + L; ++p) tab[p] = (uint16_t)g;  // pieces starting in this segment
+      seg[g] = seg_pack(adj, start + L);
+      for (; 16 * p - d0 < start + L; ++p) {  // pieces starting in this segment
+        tab[p] = (uint8_t)g;
+        if ((p & 63) == 0) tbase[p >> 6] = (uint16_t)g;
+      }
       start += L;
     }
-    if (tid + 1 == nr) seg[5 * nr] = int2{kGatherHdr, start};  // read (never used) as the last segment's successor
+    if (tid + 1 == nr) seg[5 * nr] = seg_pack(kGatherHdr, start);  // read (never used) as the last segment's successor
     if (blob_off) {
       blob_off[i] = o_first + B;
       if (i + 1 == n) blob_off[n] = o_first + start;
@@ -318,7 +335,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
       }
       ++g;
       while (pos < end) {
-        const int2 sn = seg[++g];
+        const int2 sn = seg_unpack(seg[++g]);
         if (sn.y > pos) {
           merge(*reinterpret_cast<const u32x4_ua*>(img + sn.x + x));
           pos = sn.y;
@@ -340,8 +357,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(7))) void r
     return *reinterpret_cast<const u32x4_ua*>(img + at);
   };
   for (uint32_t p = tid; p < np; p += 256) {
-    const uint32_t g = tab[p];
-    const int2 s0 = seg[g], s1 = seg[g + 1];  // the piece's segment and the next, one read
+    const uint32_t gb = tbase[p >> 6];
+    const uint32_t g = gb + ((tab[p] - gb) & 0xffu);
+    const int2 s0 = seg_unpack(seg[g]), s1 = seg_unpack(seg[g + 1]);  // the piece's segment and the next
     piece(p, g, s0, s1, window(s0, p), window(s1, p));
   }
 }
