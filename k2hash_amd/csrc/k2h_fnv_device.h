@@ -508,9 +508,9 @@ __device__ __forceinline__ void fnv_lds_round8o_last(uint32_t& lo, uint32_t& hi,
 // One round of line DMA for the line kernel: 8 global_load_lds_dwordx4, each an SGPR base
 // (`src`, wave-uniform) + the lane's 32-bit offset v[i], LDS destination m + 1024 i in M0.
 // As asm, the compiler neither counts these loads nor waits for them: every wait on them
-// is the caller's explicit s_waitcnt vmcnt.  M0 is a reserved register the compiler sets
-// before each of its own uses (it cannot be declared clobbered); the caller's kernel has
-// no other M0 user.
+// is the caller's explicit s_waitcnt vmcnt.  M0 is compiler-reserved (it cannot be
+// declared clobbered) and is not restored here: the caller's kernel must have no other M0
+// user -- tests/test_kernel_source.py checks the line-DMA kernel's code for any.
 #define K2H_DMA1(I, OFF)             \
   "s_add_u32 m0, %[m], " #OFF "\n\t" \
   "s_nop 0\n\t"                      \

@@ -60,3 +60,22 @@ def test_lines_kernel_stores_follow_all_dma_loads(csr_asm):
         assert min(stores) > max(dma), f"{sym}: a vector store precedes the last LDS-DMA load"
         waits = [s for s in ins if s.startswith("s_waitcnt") and "vmcnt(" in s]
         assert any("vmcnt(8)" in s for s in waits), f"{sym}: expected the partial vmcnt(NP*(D-1)) wait"
+
+
+def test_lines_kernel_has_no_compiler_m0_use(csr_asm):
+    """The line-DMA kernel writes M0 inside its own asm DMA statements (line_dma8) without
+    saving it.  That is only safe while hipcc itself never relies on M0 in the kernel: no
+    instruction outside the asm statements may name m0."""
+    funcs = _functions(csr_asm, "fnv_fixed_lines_kernel")
+    assert funcs
+    for sym, body in funcs:
+        inside, hits = False, []
+        for ln in body.splitlines():
+            s = ln.strip()
+            if s.startswith(";;#ASMSTART"):
+                inside = True
+            elif s.startswith(";;#ASMEND"):
+                inside = False
+            elif not inside and not s.startswith((";", ".")) and re.search(r"\bm0\b", s):
+                hits.append(s)
+        assert not hits, f"{sym}: compiler-emitted M0 use {hits[:3]}"
