@@ -290,6 +290,38 @@ __device__ __forceinline__ void fnv_key32_x2(const void* src, uint64_t* dst1, ui
                : K2H_X_CLOBBERS);
 }
 
+// Two 32-byte keys per lane, h1 only, as ONE statement: the four nt loads issued together
+// (key 0 into v[40:47], key 1 into v[32:39]), key 0 hashed as soon as ITS two loads have
+// landed (vmcnt(2): loads return in order) while key 1's are still in flight, key 1 hashed
+// in place (no copies into the window), both hashes stored at the end.  hipcc, given the
+// loads as code, waited for all four before the first hash (vmcnt(0)).
+#define K2H_X_KEY1 \
+  K2H_X_PAIR("v32", "v33", "v[32:33]") K2H_X_PAIR("v34", "v35", "v[34:35]") K2H_X_PAIR("v36", "v37", "v[36:37]") \
+      K2H_X_PAIR("v38", "v39", "v[38:39]")
+__device__ __forceinline__ void fnv_key32_pair_x(const void* src0, const void* src1, uint64_t* dst0, uint64_t* dst1,
+                                                 uint64_t seed) {
+  asm volatile("global_load_dwordx4 v[40:43], %[s0], off nt\n\t"
+               "global_load_dwordx4 v[44:47], %[s0], off offset:16 nt\n\t"
+               "global_load_dwordx4 v[32:35], %[s1], off nt\n\t"
+               "global_load_dwordx4 v[36:39], %[s1], off offset:16 nt\n\t"
+               "v_mov_b32 v48, %[slo]\n\t"
+               "v_mov_b32 v49, %[shi]\n\t"
+               "v_mov_b32 v50, 0\n\t"
+               "s_waitcnt vmcnt(2)\n\t" K2H_X_BODY K2H_X_PAIR("v46", "v47", "v[46:47]")
+               "v_mov_b32 v62, v48\n\t"
+               "v_mov_b32 v63, v49\n\t"
+               "v_mov_b32 v48, %[slo]\n\t"
+               "v_mov_b32 v49, %[shi]\n\t"
+               "s_waitcnt vmcnt(0)\n\t" K2H_X_KEY1
+               "global_store_dwordx2 %[d0], v[62:63], off nt\n\t"
+               "global_store_dwordx2 %[d1], v[48:49], off nt\n\t"
+               "s_nop 1\n\t"
+               :
+               : [s0] "v"(src0), [s1] "v"(src1), [d0] "v"(dst0), [d1] "v"(dst1), [slo] "s"((uint32_t)seed),
+                 [shi] "s"((uint32_t)(seed >> 32)), [p] "s"(kPrimeLo), [sel] "s"(kSmearSel)
+               : "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", K2H_X_CLOBBERS, "v62", "v63");
+}
+
 }  // namespace k2h
 
 // ---------------------------------------------------------------------------

@@ -114,13 +114,23 @@ static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256)
 // each wave keeps KPT*2 KiB in flight while it computes; one-wave blocks let a finished
 // wave's slot be refilled at once (round-1 A/B: KPT = 2, 64-thread blocks, nt loads and
 // stores).  The second key's registers sit below the asm window, so
-// the kernel stays at 59 VGPRs (8 waves/SIMD).
+// the kernel stays at 59 VGPRs (8 waves/SIMD).  The headline form (KPT = 2, h1 only) is one
+// asm statement per lane (fnv_key32_pair_x): hipcc waited for all four loads before the
+// first hash; there key 0 is hashed once its own two loads are in (vmcnt(2)) and key 1 in
+// the registers it was loaded into (round 3: 118.0 -> 113.7 us on config 2 in A/B,
+// profiles/r03af_fixed32_ab.txt).
 template <bool H2, int KPT, bool EPI = false>
 __global__ __launch_bounds__(64) void fnv_fixed32_kpt_kernel(const uint4* __restrict__ keys, uint64_t n,
                                                              uint64_t seed, uint64_t* __restrict__ h1,
                                                              uint64_t* __restrict__ h2, BucketParams bp = {}) {
   constexpr int BS = 64;
   const uint64_t base = (uint64_t)blockIdx.x * (BS * KPT) + threadIdx.x;
+  if constexpr (KPT == 2 && !H2 && !EPI) {  // the headline form: one asm statement per lane
+    // lanes past the end re-hash key n-1 and store its (identical) hash to h1[n-1]
+    const uint64_t i0 = base < n ? base : n - 1, i1 = base + BS < n ? base + BS : n - 1;
+    fnv_key32_pair_x(keys + 2 * i0, keys + 2 * i1, h1 + i0, h1 + i1, seed);
+    return;
+  }
   uint4 a[KPT], b[KPT];
 #pragma unroll
   for (int j = 0; j < KPT; ++j) {
