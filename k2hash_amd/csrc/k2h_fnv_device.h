@@ -322,6 +322,63 @@ __device__ __forceinline__ void fnv_key32_pair_x(const void* src0, const void* s
                : "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", K2H_X_CLOBBERS, "v62", "v63");
 }
 
+// The same two-key statement with the hashes returned in registers (stored by the caller,
+// e.g. with the fused bucket-index epilogue); H2 also returns each key's second hash (the
+// state before its last byte: key 0's parked in v55/v59 while key 1 is hashed).
+#define K2H_X_KEY1_LAST \
+  K2H_X_PAIR("v32", "v33", "v[32:33]") K2H_X_PAIR("v34", "v35", "v[34:35]") K2H_X_PAIR("v36", "v37", "v[36:37]") \
+      K2H_X_PAIR_LAST("v38", "v39", "v[38:39]")
+#define K2H_PAIR_HEAD                                   \
+  "global_load_dwordx4 v[40:43], %[s0], off nt\n\t"          \
+  "global_load_dwordx4 v[44:47], %[s0], off offset:16 nt\n\t" \
+  "global_load_dwordx4 v[32:35], %[s1], off nt\n\t"          \
+  "global_load_dwordx4 v[36:39], %[s1], off offset:16 nt\n\t" \
+  "v_mov_b32 v48, %[slo]\n\t"                                 \
+  "v_mov_b32 v49, %[shi]\n\t"                                 \
+  "v_mov_b32 v50, 0\n\t"                                      \
+  "s_waitcnt vmcnt(2)\n\t"
+#define K2H_PAIR_INPUTS                                                                                     \
+  [s0] "v"(src0), [s1] "v"(src1), [slo] "s"((uint32_t)seed), [shi] "s"((uint32_t)(seed >> 32)), [p] "s"(kPrimeLo), \
+      [sel] "s"(kSmearSel)
+template <bool H2>
+__device__ __forceinline__ void fnv_key32_pair_r(const void* src0, const void* src1, uint64_t seed, uint64_t& r0,
+                                                 uint64_t& r1, uint64_t& s0, uint64_t& s1) {
+  uint32_t a0, a1, b0, b1;
+  if constexpr (!H2) {
+    asm volatile(K2H_PAIR_HEAD K2H_X_BODY K2H_X_PAIR("v46", "v47", "v[46:47]")
+                 "v_mov_b32 v62, v48\n\t"
+                 "v_mov_b32 v63, v49\n\t"
+                 "v_mov_b32 v48, %[slo]\n\t"
+                 "v_mov_b32 v49, %[shi]\n\t"
+                 "s_waitcnt vmcnt(0)\n\t" K2H_X_KEY1
+                 : "={v62}"(a0), "={v63}"(a1), "={v48}"(b0), "={v49}"(b1)
+                 : K2H_PAIR_INPUTS
+                 : "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45",
+                   "v46", "v47", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "v60", "v61",
+                   "vcc", "memory");
+    s0 = s1 = 0;
+  } else {
+    uint32_t c0, c1, d0, d1;
+    asm volatile(K2H_PAIR_HEAD K2H_X_BODY K2H_X_PAIR_LAST("v46", "v47", "v[46:47]")
+                 "v_mov_b32 v62, v48\n\t"
+                 "v_mov_b32 v63, v49\n\t"
+                 "v_mov_b32 v55, v60\n\t"
+                 "v_mov_b32 v59, v61\n\t"
+                 "v_mov_b32 v48, %[slo]\n\t"
+                 "v_mov_b32 v49, %[shi]\n\t"
+                 "s_waitcnt vmcnt(0)\n\t" K2H_X_KEY1_LAST
+                 : "={v62}"(a0), "={v63}"(a1), "={v48}"(b0), "={v49}"(b1), "={v55}"(c0), "={v59}"(c1),
+                   "={v60}"(d0), "={v61}"(d1)
+                 : K2H_PAIR_INPUTS
+                 : "v32", "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45",
+                   "v46", "v47", "v50", "v51", "v52", "v53", "v54", "v56", "v57", "v58", "vcc", "memory");
+    s0 = ((uint64_t)c1 << 32) | c0;
+    s1 = ((uint64_t)d1 << 32) | d0;
+  }
+  r0 = ((uint64_t)a1 << 32) | a0;
+  r1 = ((uint64_t)b1 << 32) | b0;
+}
+
 }  // namespace k2h
 
 // ---------------------------------------------------------------------------

@@ -130,6 +130,21 @@ __global__ __launch_bounds__(64) void fnv_fixed32_kpt_kernel(const uint4* __rest
     const uint64_t i0 = base < n ? base : n - 1, i1 = base + BS < n ? base + BS : n - 1;
     fnv_key32_pair_x(keys + 2 * i0, keys + 2 * i1, h1 + i0, h1 + i1, seed);
     return;
+  } else if constexpr (KPT == 2) {  // h2 and / or the fused index: the same statement, hashes returned
+    const uint64_t i0 = base < n ? base : n - 1, j1 = base + BS, i1 = j1 < n ? j1 : n - 1;
+    uint64_t r0, r1, s0, s1;
+    fnv_key32_pair_r<H2>(keys + 2 * i0, keys + 2 * i1, seed, r0, r1, s0, s1);
+    if (base < n) {
+      st_nt(h1 + base, r0);
+      if constexpr (H2) st_nt(h2 + base, s0);
+      if constexpr (EPI) bucket_emit(bp, base, r0);
+    }
+    if (j1 < n) {
+      st_nt(h1 + j1, r1);
+      if constexpr (H2) st_nt(h2 + j1, s1);
+      if constexpr (EPI) bucket_emit(bp, j1, r1);
+    }
+    return;
   }
   uint4 a[KPT], b[KPT];
 #pragma unroll

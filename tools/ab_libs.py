@@ -29,6 +29,7 @@ p.add_argument("--variant", type=int, default=0)
 p.add_argument("--rounds", type=int, default=5)
 p.add_argument("--reps", type=int, default=10)
 p.add_argument("--second", action="store_true")
+p.add_argument("--index", action="store_true", help="fixed keys: the fused bucket-index form (kindex + ckindex)")
 a = p.parse_args()
 
 dev = torch.device("cuda:0")
@@ -62,6 +63,9 @@ for s in range(2 if cfg["kind"] != "ralledata" else 0):
         algo = int(off[-1].item()) + 16 * n + 8
 if a.second:
     algo += 8 * n
+if a.index:
+    algo += 16 * n
+    idx = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
 out = (torch.empty(n, dtype=torch.int64, device=dev), torch.empty(n, dtype=torch.int64, device=dev))
 
 paths = [str(_native.BATCH_LIB)] + [x for x in a.libs.split(",") if x]
@@ -83,7 +87,10 @@ def run(lib, i):
     keys, off = sets[i & 1]
     h2 = out[1].data_ptr() if a.second else None
     stream = torch.cuda.current_stream().cuda_stream
-    if off is None:
+    if off is None and a.index:
+        rc = lib.k2h_amd_hash_fixed_index(keys.data_ptr(), cfg["key_len"], n, out[0].data_ptr(), h2, 0,
+                                          (1 << 28) - 1, 0xF, idx[0].data_ptr(), idx[1].data_ptr(), stream)
+    elif off is None:
         rc = lib.k2h_amd_hash_fixed(keys.data_ptr(), cfg["key_len"], n, out[0].data_ptr(), h2, 0, stream)
     else:
         rc = lib.k2h_amd_hash_csr(keys.data_ptr(), off.data_ptr(), n, out[0].data_ptr(), h2, 0, stream)
