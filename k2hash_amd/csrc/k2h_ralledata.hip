@@ -32,6 +32,9 @@ namespace {
 typedef uint64_t u64_ua __attribute__((aligned(1)));
 typedef uint32_t u32x4_ua __attribute__((ext_vector_type(4), aligned(1)));
 
+// Workgroup barrier over LDS only (see its use in ralledata_gather_kernel).
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ uint64_t seg_len(const uint64_t* off, uint64_t i) { return off ? off[i + 1] - off[i] : 0; }
 __device__ __forceinline__ uint64_t seg_before(const uint64_t* off, uint64_t i) { return off ? off[i] - off[0] : 0; }
 
@@ -245,7 +248,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
         if (q >= before && q < before + hull_n[s]) addr = hull_lo[s] + 16 * (q - before);
         before += hull_n[s];
       }
-      v[u] = *reinterpret_cast<const u32x4_al*>((uintptr_t)addr);
+      // a global (not flat) load: hipcc must otherwise assume it may touch LDS and makes
+      // the LDS reads after the barrier wait for every vector-memory operation
+      v[u] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4_al*>((uintptr_t)addr);
       dst[u] = kGatherHdr + 80 * R + 16 * (uint32_t)q;
     }
   }
@@ -263,7 +268,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
   }
   if (tid < 16) spad[tid] = spad_tab.v[tid];
   if (tid < nr) {
-    const uint64_t i = r0 + tid;
     uint32_t rel[4], len[4];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
@@ -292,15 +296,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
       start += L;
     }
     if (tid + 1 == nr) seg[5 * nr] = seg_pack(kGatherHdr, start);  // read (never used) as the last segment's successor
-    if (blob_off) {
-      blob_off[i] = o_first + B;
-      if (i + 1 == n) blob_off[n] = o_first + start;
-    }
   }
 #pragma unroll
   for (int u = 0; u < PPT; ++u)
     if (dst[u] != 0xffffffffu) *reinterpret_cast<u32x4_al*>(img + dst[u]) = v[u];
-  __syncthreads();
+  // The block's waves share only LDS, so the two barriers wait for LDS operations alone
+  // (__syncthreads() also waits for every outstanding vector-memory operation).
+  lds_sync();
+  // the blob offsets by wave 1, idle while wave 0 hashes, from the segment table (a
+  // record's header segment ends 80 bytes after its blob starts; the sentinel holds the
+  // span's end): wave 0's critical path then carries no store whose acknowledgement a
+  // later wait would include
+  if (blob_off && tid >= 64 && tid - 64 < nr) {
+    const uint32_t r = tid - 64;
+    blob_off[r0 + r] = o_first + (uint64_t)(uint32_t)(seg_unpack(seg[5 * r]).y - 80);
+    if (r0 + r + 1 == n) blob_off[n] = o_first + (uint64_t)(uint32_t)seg_unpack(seg[5 * nr]).y;
+  }
   // 1c. wave 0 hashes the block's keys from the image into the headers
   if (tid < nr) {
     const uint32_t kl = ro1[0] - ro0[0], ke = ro1[0] - (uint32_t)sbase[0];
@@ -309,7 +320,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
     *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid) =
         u32x4_al{(uint32_t)h1, (uint32_t)(h1 >> 32), (uint32_t)h2, (uint32_t)(h2 >> 32)};
   }
-  __syncthreads();
+  lds_sync();
   // 2. aligned output pieces: the window of each segment in the piece, aligned with the
   // piece, merged forward (segment k supplies bytes [its start, 16) over what came before)
   const int32_t sp = (int32_t)span;
