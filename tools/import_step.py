@@ -3,8 +3,15 @@
 --calls calls of archive.import_scan_prehash_device.
 
     rocprofv3 ... -- python3 tools/import_step.py [--calls K]
+
+With --ab LIB: same-process A/B of the working tree's library against another build of it
+(tools/build_ab.sh), interleaved rounds, each library's result checked against
+tests/golden/import_digest.json first.
 """
 import argparse
+import ctypes
+import json
+import statistics
 import sys
 import time
 from pathlib import Path
@@ -15,15 +22,50 @@ sys.path.insert(0, str(ROOT))
 import torch  # noqa: E402
 
 import bench  # noqa: E402
-from k2hash_amd import archive  # noqa: E402
+from k2hash_amd import _native, archive  # noqa: E402
+
+
+def _verify(out):
+    recs, h1, h2 = out
+    g = json.loads((ROOT / "tests" / "golden" / "import_digest.json").read_text())
+    cols = {"key_off": recs[:, 0], "key_len": recs[:, 1], "val_off": recs[:, 2], "val_len": recs[:, 3],
+            "h1": h1, "h2": h2}
+    return g["records"] == recs.shape[0] and all(bench.digest_dev(v.contiguous(), 0) == g[k] for k, v in cols.items())
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=10)
+    ap.add_argument("--ab", default="", help="another build of libk2hash_amd.so to time against the tree's")
+    ap.add_argument("--rounds", type=int, default=9)
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     data = bench.import_workload(dev)
+    if a.ab:
+        libs = {"tree": _native.batch_lib(),
+                a.ab: _native._bind(ctypes.CDLL(str(Path(a.ab).resolve())), _native.SIGNATURES.keys())}
+        for name, lib in libs.items():
+            _native._batch = lib  # tool only: route archive's calls to this build
+            ok = _verify(archive.import_scan_prehash_device(data))
+            print(f"{name}: parity {'OK' if ok else 'MISMATCH'}", flush=True)
+            if not ok:
+                sys.exit(1)
+        times = {k: [] for k in libs}
+        for _ in range(a.rounds):
+            for name, lib in libs.items():
+                _native._batch = lib
+                for _ in range(3):
+                    archive.import_scan_prehash_device(data)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                for _ in range(a.calls):
+                    archive.import_scan_prehash_device(data)
+                torch.cuda.synchronize()
+                times[name].append((time.perf_counter() - t0) / a.calls * 1e3)
+        for name in libs:
+            print(json.dumps({"lib": name, "ms_per_call_median": statistics.median(times[name]),
+                              "ms_per_call_min": min(times[name]), "all": times[name]}), flush=True)
+        return
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < 0.15:
         archive.import_scan_prehash_device(data)
