@@ -309,3 +309,24 @@ def test_out_tensors_validated(cuda, oracle):
     h1, _ = k2hash_amd.hash_fixed(keys, 32, out=(ok, None))  # the valid form still works
     torch.cuda.synchronize()
     assert np.array_equal(host_u64(h1), oracle.hash_fixed(data, 32)[0])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 65, 130])
+def test_fixed32_writes_nothing_past_n(cuda, oracle, n):
+    """The fixed32 kernels clamp lanes past the end to key n-1 (they re-hash it and store its
+    identical hash): no output element past n may change, with or without h2 / the index."""
+    import torch
+    data = oracle.gen_bytes(32 * n, byte_off=32 * 4242)
+    r1, r2 = oracle.hash_fixed(data, 32)
+    keys = dev_u8(torch, data, cuda)
+    sentinel = -0x0123456789ABCDEF
+    bufs = [torch.full((n + 256,), sentinel, dtype=torch.int64, device=cuda) for _ in range(6)]
+    k2hash_amd.hash_fixed(keys, 32, second=False, out=(bufs[0][:n], None))
+    k2hash_amd.hash_fixed(keys, 32, second=True, out=(bufs[1][:n], bufs[2][:n]))
+    batch.hash_fixed_index(keys, 32, (1 << 28) - 1, 0xF, out=(bufs[3][:n], None, bufs[4][:n], bufs[5][:n]))
+    torch.cuda.synchronize()
+    for b, ref in ((bufs[0], r1), (bufs[1], r1), (bufs[2], r2), (bufs[3], r1)):
+        assert np.array_equal(host_u64(b[:n]), ref)
+    for b in bufs:
+        assert bool((b[n:] == sentinel).all())
