@@ -565,6 +565,7 @@ struct EntryScan {
   TState* tile_in;     // [ntile] state entering the tile
   uint32_t* done;      // tiles finished, zero between calls
   uint64_t* count;     // records in the file
+  uint64_t* host_count;  // the same, into mapped pinned host memory (no read-back copy)
   uint64_t nblk, ntile;
 };
 
@@ -700,6 +701,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_scan_kernel(EntryScan es) {
   if (threadIdx.x == 0) {
     const TState e = gapply(all, s0);
     es.count[0] = e.r + e.m;
+    __hip_atomic_store(es.host_count, e.r + e.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     es.done[0] = 0;
   }
 }
@@ -923,6 +925,8 @@ struct TsvScratch {
   void* p = nullptr;
   size_t bytes = 0;
   void* cnt = nullptr;  // done (u32) at 0, count (u64) at 8
+  uint64_t* hcnt = nullptr;   // record count, mapped pinned host memory ...
+  uint64_t* hcnt_d = nullptr;  // ... and its device address
 };
 TsvScratch g_tsv[64];
 
@@ -965,6 +969,18 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
     tr(hipMemsetAsync(sc.cnt, 0, 256, stream));
     if (e != hipSuccess) sc.cnt = nullptr;
   }
+  if (e == hipSuccess && !sc.hcnt) {  // the count comes back without a copy command
+    void* hp = nullptr;
+    tr(hipHostMalloc(&hp, 64, hipHostMallocMapped));
+    void* dp = nullptr;
+    if (e == hipSuccess) tr(hipHostGetDevicePointer(&dp, hp, 0));
+    if (e == hipSuccess) {
+      sc.hcnt = (uint64_t*)hp;
+      sc.hcnt_d = (uint64_t*)dp;
+    } else if (hp) {
+      (void)hipHostFree(hp);
+    }
+  }
   uint8_t* base = (uint8_t*)sc.p;
   uint8_t* cb = (uint8_t*)sc.cnt;
   EntryScan es;
@@ -974,6 +990,7 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   es.tile_in = (TState*)(base + o_ti);
   es.done = (uint32_t*)cb;
   es.count = (uint64_t*)(cb + 8);
+  es.host_count = sc.hcnt_d;
   es.nblk = nblk;
   es.ntile = ntile;
   uint64_t* dcount = es.count;
@@ -999,9 +1016,8 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
                                                                     nullptr);
     e = hipGetLastError();
   }
-  uint64_t n = 0;
-  tr(hipMemcpyAsync(&n, dcount, 8, hipMemcpyDeviceToHost, stream));
   tr(hipStreamSynchronize(stream));
+  const uint64_t n = e == hipSuccess ? __atomic_load_n(sc.hcnt, __ATOMIC_ACQUIRE) : 0;
   if (sc.bytes > kScratchKeep) {  // the stream is synchronised: no kernel still reads it
     (void)hipFree(sc.p);
     sc.p = nullptr;
