@@ -286,3 +286,40 @@ def test_device_scan_over_4gib_tile_scan_runs(cuda):
         assert torch.equal(part[:, 0] - c * size, r1[:, 0]) and torch.equal(part[:, 2] - c * size, r1[:, 2]), c
         assert torch.equal(part[:, 1], r1[:, 1]) and torch.equal(part[:, 3], r1[:, 3]), c
         assert torch.equal(a4[c * n:(c + 1) * n], a1) and torch.equal(b4[c * n:(c + 1) * n], b1), c
+
+
+@pytest.mark.gpu
+def test_fused_scan_prehash_concurrent_threads(cuda, oracle):
+    """Calls from several host threads at once (the per-device scratch and the mapped record
+    count are shared under a lock): every call returns its own file's records and hashes."""
+    import concurrent.futures
+    import torch
+
+    rng = np.random.default_rng(11)
+    files = []
+    for n in (700, 1500, 2300, 3100):
+        lines = [b"k%d-" % i + bytes(rng.integers(97, 123, int(rng.integers(1, 40))).astype(np.uint8)) + b"\t" +
+                 bytes(rng.integers(97, 123, int(rng.integers(0, 60))).astype(np.uint8)) + b"\n" for i in range(n)]
+        data = b"".join(lines)
+        host = archive.import_scan(data, "tsv")
+        keys = [data[int(o):int(o) + int(n)] + b"\0" for o, n in zip(host["key_off"], host["key_len"])]
+        hh1 = np.array([oracle.k2h_hash(k) for k in keys], np.uint64)  # K2HShm::Set(const char*): key + NUL
+        hh2 = np.array([oracle.k2h_second_hash(k) for k in keys], np.uint64)
+        files.append((data, host, (hh1, hh2)))
+
+    def work(k):
+        data, host, (hh1, hh2) = files[k]
+        f = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda)
+        for _ in range(5):
+            recs, h1, h2 = archive.import_scan_prehash_device(f, "tsv")
+            torch.cuda.synchronize()
+            a = recs.cpu().numpy().view(np.uint64)
+            assert a.shape[0] == host.size
+            for i, name in enumerate(archive.IMPORT_DTYPE.names):
+                assert np.array_equal(a[:, i], host[name])
+            assert np.array_equal(h1.cpu().numpy().view(np.uint64), hh1)
+            assert np.array_equal(h2.cpu().numpy().view(np.uint64), hh2)
+        return True
+
+    with concurrent.futures.ThreadPoolExecutor(4) as ex:
+        assert all(ex.map(work, range(4)))
