@@ -292,6 +292,8 @@ def hash_csr_index_table(data, offsets, cur_mask: int, collision_mask: int, assi
     n = offsets.numel() - 1
     if n < 0:
         raise ValueError("offsets must have n+1 entries")
+    if offsets.device != data.device:
+        raise ValueError("data and offsets must be on one device")
     tab = _table(torch, cur_mask, collision_mask, assigned, data.device)
     h1 = torch.empty(n, dtype=torch.int64, device=data.device)
     h2 = torch.empty(n, dtype=torch.int64, device=data.device) if second else None

@@ -352,6 +352,26 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_index(const void* by
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_csr (index)", e);
 }
 
+// Table forms with a NULL bitmap (every entry assigned) run the stateless epilogue; what
+// that epilogue cannot express is filled here: found = 1 (0 when cur_mask is 0), and for
+// cur_mask 0 kindex = K2H_AMD_KINDEX_NONE -- GetKIndex returns NULL then
+// (lib/k2hshm.cc:882-907), the same as the bitmap form -- so the epilogue
+// does not write kindex in that case.
+static int null_bitmap_fill(const k2h_amd_table* table, uint64_t n, uint64_t* kindex, uint8_t* found,
+                            k2h::BucketParams& bp, void* stream) {
+  if (table->assigned) return K2H_AMD_OK;
+  if (found) {
+    hipError_t e = hipMemsetAsync(found, table->cur_mask ? 1 : 0, n, (hipStream_t)stream);
+    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "found fill", e);
+  }
+  if (kindex && table->cur_mask == 0) {
+    hipError_t e = hipMemsetAsync(kindex, 0xFF, n * sizeof(uint64_t), (hipStream_t)stream);
+    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "kindex fill", e);
+    bp.kindex = nullptr;
+  }
+  return K2H_AMD_OK;
+}
+
 __attribute__((visibility("default"))) int k2h_amd_bucket_index_table(const uint64_t* h1, uint64_t n,
                                                                       const k2h_amd_table* table, uint64_t* kindex,
                                                                       uint64_t* ckindex, uint8_t* found, void* stream) {
@@ -363,10 +383,7 @@ __attribute__((visibility("default"))) int k2h_amd_bucket_index_table(const uint
   if (rc) return rc;
   bp.assigned = table->assigned;
   bp.found = table->assigned ? found : nullptr;
-  if (found && !table->assigned) {  // every entry assigned: found is all ones unless cur_mask is 0
-    hipError_t e = hipMemsetAsync(found, table->cur_mask ? 1 : 0, n, (hipStream_t)stream);
-    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "found fill", e);
-  }
+  if ((rc = null_bitmap_fill(table, n, kindex, found, bp, stream))) return rc;
   hipError_t e = k2h::launch_bucket_index(h1, n, bp, (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_bucket_index (table)", e);
 }
@@ -383,10 +400,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed_index_table(
   if (rc) return rc;
   bp.assigned = table->assigned;
   bp.found = table->assigned ? found : nullptr;
-  if (found && !table->assigned) {
-    hipError_t e = hipMemsetAsync(found, table->cur_mask ? 1 : 0, n, (hipStream_t)stream);
-    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "found fill", e);
-  }
+  if ((rc = null_bitmap_fill(table, n, kindex, found, bp, stream))) return rc;
   hipError_t e = k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_fixed (table index)", e);
 }
@@ -402,10 +416,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_index_table(
   if (rc) return rc;
   bp.assigned = table->assigned;
   bp.found = table->assigned ? found : nullptr;
-  if (found && !table->assigned) {
-    hipError_t e = hipMemsetAsync(found, table->cur_mask ? 1 : 0, n, (hipStream_t)stream);
-    if (e != hipSuccess) return fail(K2H_AMD_EHIP, "found fill", e);
-  }
+  if ((rc = null_bitmap_fill(table, n, kindex, found, bp, stream))) return rc;
   hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_csr (table index)", e);
 }

@@ -339,3 +339,21 @@ def test_table_index_null_bitmap_is_stateless(cuda, oracle):
     assert torch.equal(k, ks) and torch.equal(c, cs) and bool((f == 1).all())
     with pytest.raises(ValueError):  # bitmap shorter than cur_mask + 1 bits
         batch.bucket_index_table(th, 0xFFFF, 0xF, torch.zeros(100, dtype=torch.int32, device=cuda))
+    # cur_mask 0: GetKIndex returns NULL (lib/k2hshm.cc:882-907) -> K2H_AMD_KINDEX_NONE and
+    # found 0, the same with a NULL bitmap as with an all-ones one, in the
+    # standalone and both fused forms
+    ones = torch.full((1,), -1, dtype=torch.int32, device=cuda)
+    keys = torch.from_numpy(oracle.gen_bytes(32 * 5000)).to(cuda)
+    off = oracle.gen_offsets(3000, 0, 200)
+    cdata = torch.from_numpy(oracle.gen_bytes(int(off[-1]))).to(cuda)
+    coff = torch.from_numpy(off.astype(np.int64)).to(cuda)
+    for assigned in (None, ones):
+        outs = [batch.bucket_index_table(th, 0, 0xF, assigned)[:3],
+                batch.hash_fixed_index_table(keys, 32, 0, 0xF, assigned)[2:],
+                batch.hash_csr_index_table(cdata, coff, 0, 0xF, assigned)[2:]]
+        torch.cuda.synchronize()
+        for k0, c0, f0 in outs:
+            assert bool((k0 == -1).all()) and bool((f0 == 0).all()), assigned
+    # offsets on another device than the bytes: rejected before any launch
+    with pytest.raises(ValueError):
+        batch.hash_csr_index_table(cdata, coff.cpu(), 0xFF, 0xF)
