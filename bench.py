@@ -86,7 +86,9 @@ def parse(argv=None):
     p.add_argument("--rehearse-cpu", action="store_true",
                    help="no GPU: run the launcher / shard / gather path on CPU with the scalar plugin "
                         "(a rehearsal of the N>1 plumbing, not a measurement)")
-    p.add_argument("--keys", type=int, default=0, help="override keys per rank (tests / rehearsals)")
+    p.add_argument("--keys", type=int, default=0,
+                   help="override the key count (tests / rehearsals): keys per rank for the weak configs, "
+                        "the whole batch for the sharded ones (fixed32_1g; csr at N > 1 or with --dist)")
     p.add_argument("--child-timeout", type=float, default=540.0,
                    help="self-launcher: kill every rank after this long (below the driver's 600 s limit)")
     p.add_argument("--init-timeout", type=float, default=180.0,
@@ -325,6 +327,14 @@ def _golden():
 
 
 def digest_dev(h, first: int) -> list[str]:
+    return [f"{v:016x}" for v in digest_ints(h, first)]
+
+
+def digest_ints(h, first: int) -> list[int]:
+    """[xor, wrapping sum, wrapping sum of h * (2 i + 1)] of the hashes h of global keys
+    first .. first + h.numel() - 1, as unsigned 64-bit ints.  Each term is a xor or a sum
+    over keys, so the digest of a key range is the combination (xor, +, +) of the digests of
+    any partition of it -- how sharded results are checked without gathering them."""
     import torch
 
     x = h
@@ -338,7 +348,46 @@ def digest_dev(h, first: int) -> list[str]:
     s = int(h.sum().item())
     w = 2 * (torch.arange(h.numel(), dtype=torch.int64, device=h.device) + first) + 1
     ws = int((h * w).sum().item())
-    return [f"{v & (2**64 - 1):016x}" for v in (xr, s, ws)]
+    return [v & (2**64 - 1) for v in (xr, s, ws)]
+
+
+def verify_sharded(h, first: int, chunks, dist=None, dev=None) -> dict:
+    """Check reference chunks against hashes spread over the ranks: each rank digests the
+    part of every chunk that lies in its key range [first, first + h.numel()) (zeros --
+    the identity -- elsewhere), the parts are all-gathered and combined (xor, +, +) and
+    every chunk wholly covered by the ranks is compared with the reference's digest.  Byte
+    cuts (CSR) do not align with the reference's chunks, so no rank holds one whole."""
+    import torch
+
+    n = h.numel()
+    parts = torch.zeros(len(chunks), 4, dtype=torch.int64)
+    for j, c in enumerate(chunks):
+        a, b = max(c["first"], first), min(c["first"] + c["count"], first + n)
+        if a < b:
+            d = digest_ints(h[a - first:b - first], a)
+            parts[j, :3] = torch.tensor([v - (1 << 64) if v >= 1 << 63 else v for v in d], dtype=torch.int64)
+            parts[j, 3] = b - a
+    allp = [parts]
+    if dist is not None and dist.is_initialized():
+        gloo = dist.get_backend() == "gloo"
+        mine = parts if gloo else parts.to(dev)
+        allp = [torch.zeros_like(mine) for _ in range(dist.get_world_size())]
+        dist.all_gather(allp, mine)
+        allp = [t.cpu() for t in allp]
+    ok, checked = True, 0
+    for j, c in enumerate(chunks):
+        xr = sm = ws = covered = 0
+        for t in allp:
+            v = [int(x) & (2**64 - 1) for x in t[j, :3].tolist()]
+            xr ^= v[0]
+            sm = (sm + v[1]) & (2**64 - 1)
+            ws = (ws + v[2]) & (2**64 - 1)
+            covered += int(t[j, 3])
+        if covered == c["count"]:
+            ok &= [f"{v:016x}" for v in (xr, sm, ws)] == c["h1"]
+            checked += 1
+    return {"chunks_checked": checked, "ok": bool(ok) and checked > 0, "ranks": len(allp),
+            "how": "per-rank partial digests of every reference chunk, all-gathered and combined"}
 
 
 def verify_chunks(h, first: int, chunks) -> dict:
@@ -350,6 +399,57 @@ def verify_chunks(h, first: int, chunks) -> dict:
             ok &= digest_dev(h[a - first:b - first], a) == c["h1"]
             checked += 1
     return {"chunks_checked": checked, "ok": bool(ok)}
+
+
+def golden_chunks(kind: str, shape, total: int):
+    """The reference digests' chunks for a whole workload of `total` keys of this kind
+    (tests/golden/digests.json), or None when the reference has none at that size."""
+    for g in _golden().values():
+        if g["n"] != total or g["kind"] != kind:
+            continue
+        if (kind == "fixed" and g["key_len"] == shape) or (kind == "csr" and (g["min_len"], g["max_len"]) == tuple(shape)):
+            return g.get("chunks") or [dict(first=0, count=g["n"], h1=g["h1"])]
+    return None
+
+
+def measure_gather(h, counts, step, gsteps: int, dist, dev, sync=lambda: None) -> tuple[dict, object]:
+    """The path's one exchange: every rank's hashes to rank 0 (shard.gather_hashes,
+    RCCL point-to-point over xGMI, or gloo), timed alone and back to back with the hash step.
+    Max over ranks.  Returns (the line's `gather` object without verify_root, rank 0's result)."""
+    import torch
+
+    from k2hash_amd import shard
+
+    res = None
+    for _ in range(2):
+        res = shard.gather_hashes(h, counts=counts)
+    sync()
+    dist.barrier()
+    g0 = time.perf_counter()
+    for _ in range(gsteps):
+        res = shard.gather_hashes(h, counts=counts)
+    sync()
+    dist.barrier()
+    gs = torch.tensor([(time.perf_counter() - g0) / gsteps], dtype=torch.float64, device=dev)
+    dist.all_reduce(gs, op=dist.ReduceOp.MAX)
+    gather_s = float(gs.item())
+    dist.barrier()  # hash + gather back to back (the end-to-end step of a bulk loader)
+    sync()
+    c0 = time.perf_counter()
+    for _ in range(gsteps):
+        step(0)
+        res = shard.gather_hashes(h, counts=counts)
+    sync()
+    dist.barrier()
+    cs = torch.tensor([(time.perf_counter() - c0) / gsteps], dtype=torch.float64, device=dev)
+    dist.all_reduce(cs, op=dist.ReduceOp.MAX)
+    combo_s = float(cs.item())
+    to_root = 8 * (sum(counts) - counts[0])
+    return {"backend": dist.get_backend(), "counts": list(counts), "ms_per_gather": gather_s * 1e3,
+            "bytes_to_root": to_root, "root_recv_gb_per_s": to_root / gather_s / 1e9,
+            "p2p_peers_at_root": sum(1 for c in counts[1:] if c),
+            "with_gather": {"ms_per_step": combo_s * 1e3, "value": sum(counts) / combo_s,
+                            "unit": "key hashes/s (hashed and gathered at rank 0)"}}, res
 
 
 # --------------------------------------------------------------------------------------
@@ -699,6 +799,11 @@ def secondary_host(dev, reps=5):
 # Rehearsal of the N > 1 plumbing without a GPU (scalar plugin hashes, gloo gather)
 # --------------------------------------------------------------------------------------
 def rehearse_cpu(args, world, rank):
+    """The N > 1 path without a GPU: the same sharding (equal key counts for fixed keys,
+    byte cuts of one CSR batch for --config csr), the same barrier-bracketed timing and MAX
+    all-reduce, the same gather measurement (measure_gather: counts, bytes_to_root, one
+    point-to-point receive per peer at the root) and the same sharded digest check
+    (verify_sharded), over gloo, with the scalar plugin hashing each rank's keys."""
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -712,18 +817,32 @@ def rehearse_cpu(args, world, rank):
                             timeout=datetime.timedelta(seconds=args.init_timeout))
     if rank == args.inject_rank_failure:
         os._exit(3)  # TEST ONLY (--inject-rank-failure): die before the first collective
+    csr = args.config == "csr"
     total = args.keys or 4096
-    first, last = shard.shard_range(total, rank, world)
-    raw = np.random.default_rng(1234).integers(0, 256, size=total * 32, dtype=np.uint8)[first * 32:last * 32]
+    rng = np.random.default_rng(1234)
+    if csr:  # one batch of 8-256 B keys (plus some empty ones), cut by bytes
+        lens = rng.integers(8, 257, size=total)
+        lens[::61] = 0
+        offs = np.zeros(total + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        cuts = shard.csr_cuts(offs, world)
+        raw = rng.integers(0, 256, size=int(offs[-1]), dtype=np.uint8)
+        keys = [raw[offs[i]:offs[i + 1]].tobytes() for i in range(total)]
+    else:
+        cuts = [shard.shard_range(total, r, world) for r in range(world)]
+        raw = rng.integers(0, 256, size=total * 32, dtype=np.uint8)
+        keys = [raw[i * 32:(i + 1) * 32].tobytes() for i in range(total)]
+    first, last = cuts[rank]
+    mine = keys[first:last]
     h = None
 
     def step(_):
         nonlocal h
-        h = torch.tensor([k2hash_amd.k2h_hash(raw[i * 32:(i + 1) * 32].tobytes()) for i in range(last - first)],
-                         dtype=torch.uint64).view(torch.int64)
+        h = torch.tensor([k2hash_amd.k2h_hash(k) for k in mine], dtype=torch.uint64).view(torch.int64)
 
     for i in range(args.warmup):
         step(i)
+    step(0)
     dist.barrier()
     t0 = time.perf_counter()
     for i in range(args.steps):
@@ -731,19 +850,29 @@ def rehearse_cpu(args, world, rank):
     dist.barrier()
     el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
     dist.all_reduce(el, op=dist.ReduceOp.MAX)
-    out = shard.gather_hashes(h, counts=shard.shard_counts(total, world))
+    # the reference chunks here: the oracle-free product scalar hash over 4 equal key ranges
+    ref = [k2hash_amd.k2h_hash(k) for k in keys]
+    ref_t = torch.tensor(ref, dtype=torch.uint64).view(torch.int64)
+    q = max(1, total // 4)
+    chunks = [dict(first=a, count=min(q, total - a), h1=digest_dev(ref_t[a:a + q], a)) for a in range(0, total, q)]
+    verify = verify_sharded(h, first, chunks, dist)
+    counts = [b - a for a, b in cuts]
+    gather, res = measure_gather(h, counts, step, 2, dist, None)
     if rank == 0:
-        ref = [k2hash_amd.k2h_hash(np.random.default_rng(1234).integers(0, 256, size=total * 32, dtype=np.uint8)
-                                   [i * 32:(i + 1) * 32].tobytes()) for i in range(total)]
-        ok = out.view(torch.uint64).tolist() == ref
+        ok = res.view(torch.uint64).tolist() == ref
+        gather["ok"] = ok
+        gather["verify_root"] = verify_chunks(res, 0, chunks)
+        if csr:
+            gather["shard_key_bytes"] = [int(offs[b] - offs[a]) for a, b in cuts]
         print(json.dumps({"metric": METRIC, "value": total * args.steps / float(el.item()), "unit": "key hashes/s",
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                           "ms_per_step": float(el.item()) / args.steps * 1e3, "higher_is_better": True,
                           "scaling": "strong", "vs_baseline": None, "dtype": "u64 (u8 key bytes in)",
                           "data": "synthetic", "device": "cpu rehearsal (scalar plugin; NOT a measurement)",
-                          "config": {"workload": f"{total} x 32B keys sharded over {world} ranks",
-                                     "parallelism": f"shard{world}"},
-                          "gather": {"ok": ok, "backend": dist.get_backend()}}), flush=True)
+                          "config": {"workload": (f"one batch of {total} CSR keys cut by bytes over {world} ranks"
+                                                  if csr else f"{total} x 32B keys sharded over {world} ranks"),
+                                     "keys_total": total, "parallelism": f"shard{world}"},
+                          "verify": verify, "gather": gather}), flush=True)
     dist.destroy_process_group()
 
 
@@ -782,15 +911,28 @@ def main():
             os._exit(3)  # TEST ONLY (--inject-rank-failure): die before the first collective
 
     # --- synthetic input: this rank's global key range -----------------------------------
-    strong = n is None
+    # Sharded configs (strong scaling, one batch over the ranks): config 4 (fixed32_1g, 2^30
+    # keys, equal key counts) and, at N > 1 or with --dist, config 3 (csr: ONE batch of 2^26
+    # keys cut by BYTES, SURVEY 8e -- shard.csr_cuts over the batch's offsets, each rank's
+    # offsets rebased to its own bytes).  Weak configs: every rank its own batch of n keys.
+    strong = n is None or (kind == "csr" and use_dist)
+    cuts = None
+    total = None
     if strong:
-        first, last = shard.shard_range(KEYS_1G, rank, world)
+        total = args.keys or (KEYS_1G if n is None else n)
+        if kind == "csr":
+            off_g = batch.synth_offsets(total, dev, shape[0], shape[1])  # the whole batch's offsets
+            cuts = shard.csr_cuts(off_g, world)
+            cut_bytes = [int(off_g[b].item()) - int(off_g[a].item()) for a, b in cuts]
+            first, last = cuts[rank]
+        else:
+            first, last = shard.shard_range(total, rank, world)
         n = last - first
     else:
         first = rank * n
-    if args.keys:
-        n = args.keys
-    nsets = 1 if strong else 2  # config 4's shards (>= 4 GiB) dwarf the 256 MiB Infinity Cache
+        if args.keys:
+            n = args.keys
+    nsets = 1 if strong else 2  # sharded batches (config 4: >= 4 GiB per rank) dwarf the 256 MiB Infinity Cache
     sets, algo_bytes, key_bytes = [], 0, 0
     for s in range(nsets):
         base = first + s * world * n  # set 0 is the rank's shard of the reference workload
@@ -810,6 +952,14 @@ def main():
             # minimal traffic: key + value bytes and their offsets in, blobs + blob offsets out
             algo_bytes = max(algo_bytes, (kb + vb + 16 * (n + 1)) + (80 * n + kb + vb + 8 * (n + 1)))
             key_bytes = max(key_bytes, kb)
+        elif strong:  # this rank's byte range of the one reference batch (byte stream offset = its first byte)
+            off = shard.rebase_offsets(off_g, first, last).contiguous()
+            b0 = int(off_g[first].item())
+            del off_g
+            nb = int(off[-1].item())
+            data = batch.synth_bytes(nb, dev, byte_off=b0)
+            sets.append((data, off))
+            algo_bytes, key_bytes = nb + 8 * n + 8 * (n + 1), nb
         else:
             off = batch.synth_offsets(n, dev, shape[0], shape[1], first_key=base)
             nb = int(off[-1].item())
@@ -846,13 +996,17 @@ def main():
             k2hash_amd.hash_csr(keys, off, second=args.second, out=outs[i % nsets])
 
     elapsed, kern_s, extra = timed(step, args.steps, args.warmup, args.warm_ms, world, dist, dev)
-    total_keys = n * world * args.steps
+    total_keys = (total if strong else n * world) * args.steps
     value = total_keys / elapsed
 
     # --- verification against the reference's digests (outside the timed region) ---------
     verify = None
-    if not args.no_verify and kind == "fixed" and not args.keys:
-        gname = {"fixed32": "fixed32_16M", "fixed32_1g": "fixed32_1G", "fixed4096": "fixed4096_1M"}[name]
+    if not args.no_verify and strong:
+        chunks = golden_chunks(kind, shape, total)
+        if chunks:
+            verify = verify_sharded(outs[0][0], first, chunks, dist if use_dist else None, dev)
+    elif not args.no_verify and kind == "fixed" and not args.keys:
+        gname = {"fixed32": "fixed32_16M", "fixed4096": "fixed4096_1M"}[name]
         g = _golden()[gname]
         if name == "fixed32":  # set 0 of rank 0 is exactly the reference's 16M-key workload
             verify = {"ok": rank != 0 or digest_dev(outs[0][0], 0) == g["h1"], "chunks_checked": 1}
@@ -863,46 +1017,24 @@ def main():
             dist.all_reduce(t)
             verify = {"ok": int(t[0].item()) == 0, "chunks_checked": int(t[1].item()), "ranks": world}
 
-    # --- config 4: the RCCL gather of every shard's hashes to rank 0 ------------------------
+    # --- the gather of every shard's hashes to rank 0 (RCCL over xGMI) ---------------------
     gather = None
     if use_dist:
-        counts = shard.shard_counts(KEYS_1G, world) if strong and not args.keys else [n] * world
-        h = outs[0][0]
+        if cuts is not None:
+            counts = [b - a for a, b in cuts]
+        elif strong:
+            counts = shard.shard_counts(total, world)
+        else:
+            counts = [n] * world
         gsteps = max(3, min(10, args.steps // 10))
-        res = None
-        for _ in range(2):
-            res = shard.gather_hashes(h, counts=counts)
-        torch.cuda.synchronize()
-        dist.barrier()
-        g0 = time.perf_counter()
-        for _ in range(gsteps):
-            res = shard.gather_hashes(h, counts=counts)
-        torch.cuda.synchronize()
-        dist.barrier()
-        gs = torch.tensor([(time.perf_counter() - g0) / gsteps], dtype=torch.float64, device=dev)
-        dist.all_reduce(gs, op=dist.ReduceOp.MAX)
-        gather_s = float(gs.item())
-        # hash + gather back to back (the end-to-end step of a bulk loader)
-        dist.barrier()
-        torch.cuda.synchronize()
-        c0 = time.perf_counter()
-        for i in range(gsteps):
-            step(0)
-            res = shard.gather_hashes(h, counts=counts)
-        torch.cuda.synchronize()
-        dist.barrier()
-        cs = torch.tensor([(time.perf_counter() - c0) / gsteps], dtype=torch.float64, device=dev)
-        dist.all_reduce(cs, op=dist.ReduceOp.MAX)
-        combo_s = float(cs.item())
-        gok = None
-        if rank == 0 and not args.no_verify and strong and not args.keys:
-            gok = verify_chunks(res, 0, _golden()["fixed32_1G"]["chunks"])
-        gather = {"backend": dist.get_backend(), "ms_per_gather": gather_s * 1e3,
-                  "bytes_to_root": 8 * (sum(counts) - counts[0]),
-                  "root_recv_gb_per_s": 8 * (sum(counts) - counts[0]) / gather_s / 1e9,
-                  "with_gather": {"ms_per_step": combo_s * 1e3, "value": sum(counts) / combo_s,
-                                  "unit": "key hashes/s (hashed and gathered at rank 0)"},
-                  "verify_root": gok}
+        gather, res = measure_gather(outs[0][0], counts, step, gsteps, dist, dev, torch.cuda.synchronize)
+        if rank == 0 and not args.no_verify and strong:
+            chunks = golden_chunks(kind, shape, total)
+            gather["verify_root"] = verify_chunks(res, 0, chunks) if chunks else None
+        else:
+            gather["verify_root"] = None
+        if cuts is not None:
+            gather["shard_key_bytes"] = cut_bytes  # the byte cuts: ~equal key bytes per rank
         del res
 
     secondary = None
@@ -952,7 +1084,9 @@ def main():
             "vs_baseline": None,
             "dtype": "u64 (u8 key bytes in)",
             "data": "synthetic (splitmix64 counter stream, generated on device; SURVEY.md 8d spec in DESIGN.md)",
-            "config": {"workload": desc, "keys_per_gpu": n, "keys_total": n * world,
+            "config": {"workload": desc + (f" -- one batch of {total} keys cut by bytes over {world} ranks"
+                                           if cuts is not None else ""),
+                       "keys_per_gpu": n, "keys_total": total if strong else n * world,
                        "key_len": shape if kind == "fixed" else list(shape),
                        "second_hash": bool(args.second), "bucket_index": bool(args.index),
                        "parallelism": f"shard{world}"},

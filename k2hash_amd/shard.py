@@ -23,13 +23,19 @@ def shard_range(n: int, rank: int, world: int) -> tuple[int, int]:
     return first, first + q + (1 if rank < r else 0)
 
 
-def shard_csr_by_bytes(offsets: np.ndarray, rank: int, world: int) -> tuple[int, int]:
+def shard_csr_by_bytes(offsets, rank: int, world: int) -> tuple[int, int]:
     """Key range [first, last) of rank `rank` such that every rank gets about the same
-    number of key BYTES (CSR keys differ in length).  Cuts fall on key boundaries."""
-    offsets = np.asarray(offsets)
-    n = offsets.size - 1
+    number of key BYTES (CSR keys differ in length).  Cuts fall on key
+    boundaries: cut k is the first key that starts at or after byte (total * k / world), so
+    a run of zero-length keys at a cut goes to the later rank.  `offsets` (n + 1 entries,
+    non-decreasing, need not start at 0) is a numpy array or a torch tensor (a device
+    tensor is searched on its device)."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError("bad rank/world")
+    is_torch = not isinstance(offsets, np.ndarray) and hasattr(offsets, "is_cuda")
+    if not is_torch:
+        offsets = np.asarray(offsets)
+    n = (offsets.numel() if is_torch else offsets.size) - 1
     lo, hi = int(offsets[0]), int(offsets[-1])
 
     def cut(k: int) -> int:
@@ -38,13 +44,25 @@ def shard_csr_by_bytes(offsets: np.ndarray, rank: int, world: int) -> tuple[int,
         if k >= world:
             return n
         target = lo + (hi - lo) * k // world
+        if is_torch:
+            import torch
+
+            t = torch.tensor([target], dtype=offsets.dtype, device=offsets.device)
+            return int(torch.searchsorted(offsets[:-1], t, side="left").item())
         return int(np.searchsorted(offsets[:-1], target, side="left"))
 
     return cut(rank), cut(rank + 1)
 
 
+def csr_cuts(offsets, world: int) -> list:
+    """Every rank's [first, last) of shard_csr_by_bytes (rank order)."""
+    return [shard_csr_by_bytes(offsets, r, world) for r in range(world)]
+
+
 def rebase_offsets(offsets, first: int, last: int):
-    """Offsets of keys [first, last) relative to their first byte (n_local + 1 entries)."""
+    """Offsets of keys [first, last) relative to their first byte (n_local + 1 entries):
+    with the bytes [offsets[first], offsets[last]) as the shard's own buffer, they index it
+    from 0.  numpy array or torch tensor in, the same kind out."""
     sub = offsets[first:last + 1]
     return sub - sub[0]
 

@@ -39,6 +39,45 @@ def test_launcher_rehearsal_cpu_three_ranks():
     assert line["n_gpus"] == 3 and line["gather"]["ok"] is True
 
 
+def _torchrun(nproc, args, timeout):
+    """The driver's N > 1 command form: python -m torch.distributed.run --nnodes=1
+    --nproc-per-node N --master-addr 127.0.0.1 --master-port P bench.py --gpus N ..."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    p = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), str(ROOT / "bench.py"),
+                        "--gpus", str(nproc)] + args, capture_output=True, text=True, timeout=timeout, env=env)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("config", ["fixed32_1g", "csr"])
+def test_rehearsal_eight_ranks_driver_command_form(config):
+    """the full N = 8 command form the driver uses, rehearsed on CPU (gloo,
+    scalar plugin): eight ranks, the per-rank counts, bytes_to_root, seven point-to-point
+    receives at the root, the sharded digest check and the gathered vector; for csr one
+    batch cut by bytes (shard_key_bytes balanced, counts uneven)."""
+    total = 4000
+    line = _torchrun(8, ["--rehearse-cpu", "--config", config, "--steps", "1", "--warmup", "0",
+                         "--keys", str(total)], 300)
+    g = line["gather"]
+    assert line["n_gpus"] == 8 and line["scaling"] == "strong" and line["config"]["keys_total"] == total
+    assert len(g["counts"]) == 8 and sum(g["counts"]) == total and g["p2p_peers_at_root"] == 7
+    assert g["bytes_to_root"] == 8 * (total - g["counts"][0])
+    assert g["ok"] is True and g["verify_root"]["ok"] is True
+    assert line["verify"]["ok"] is True and line["verify"]["ranks"] == 8
+    if config == "csr":
+        kb = g["shard_key_bytes"]
+        assert len(kb) == 8 and max(kb) - min(kb) <= 2 * 256
+
+
 def test_launcher_fails_fast_when_a_rank_dies():
     """A rank that dies after joining the process group (--inject-rank-failure, test only)
     must end the whole run with a non-zero status well inside the driver's limit, with no
@@ -90,7 +129,7 @@ def test_bench_two_ranks_one_gpu():
     assert line["gather"]["with_gather"]["value"] > 0 and line["gather"]["backend"] == "gloo"
     # profile-derived fields are scaled to this launch's key count
     rf = line["roofline"]
-    assert rf["keys_per_launch"] == 262144
+    assert rf["keys_per_launch"] == 131072  # --keys is the whole sharded batch
     assert 0 < rf["valu_frac"] < 1.2
     assert rf["traffic"] is None or rf["traffic"] / rf["algorithmic_bytes_per_launch"] < 1.2
 
@@ -184,3 +223,29 @@ def test_cpu_baseline_workload_csr_and_fixed(oracle):
     bad = f1.copy()
     bad[3] ^= 1
     assert bench.cpu_baseline_workload("fixed", keys, None, 4096, 8, 64, bad)["digest_matches_gpu"] is False
+
+
+@pytest.mark.gpu
+def test_bench_csr_two_ranks_one_batch_cut_by_bytes():
+    """bench.py --config csr at N = 2 (two ranks sharing cuda:0 over gloo)
+    strong-scales ONE config-3-shaped batch cut by bytes: the reference's 64K-key CSR
+    workload (tests/golden/digests.json csr_8_256_64K), each rank hashing its rebased shard
+    with the HIP kernel; the per-rank partial digests combine to the reference's and the
+    gathered vector at rank 0 matches it too."""
+    line = _run(["--gpus", "2", "--backend", "gloo", "--config", "csr", "--keys", "65536", "--steps", "5",
+                 "--warmup", "1", "--warm-ms", "5"], 600)
+    g = line["gather"]
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["config"]["keys_total"] == 65536
+    assert line["verify"]["ok"] is True and line["verify"]["chunks_checked"] == 1
+    assert g["verify_root"]["ok"] is True and sum(g["counts"]) == 65536
+    kb = g["shard_key_bytes"]
+    assert abs(kb[0] - kb[1]) <= 2 * 256
+
+
+@pytest.mark.gpu
+def test_bench_csr_rccl_one_rank():
+    """The driver's command form with RCCL at one rank for the CSR strong path (--dist)."""
+    line = _torchrun(1, ["--dist", "--config", "csr", "--keys", "65536", "--steps", "5", "--warmup", "1",
+                         "--warm-ms", "5"], 600)
+    assert line["gather"]["backend"] == "nccl" and line["verify"]["ok"] is True
+    assert line["gather"]["verify_root"]["ok"] is True

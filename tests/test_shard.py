@@ -51,6 +51,34 @@ def _free_port():
     return p
 
 
+def _csr_batch(world: int, n: int = 30011):
+    """One CSR batch (numpy uint64 offsets, uint8 bytes) with zero-length keys, built so
+    that shard_csr_by_bytes puts a run of zero-length keys exactly on a cut: the first
+    half's bytes equal the second half's, so the world-2 cut target is the first zero-length
+    key's start; other world sizes cut through random lengths that include zeros."""
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "oracle"))
+    import oracle
+    rng = np.random.default_rng(4242)
+    half = n // 2 - 3
+    l1 = rng.integers(0, 300, size=half)
+    l1[::97] = 0
+    l2 = rng.integers(0, 300, size=n - half - 5)
+    l2[::89] = 0
+    l2[-1] += int(l1.sum() - l2.sum())  # the two halves hold the same bytes
+    while l2[-1] < 0:  # keep lengths non-negative: spread the deficit backwards
+        j = int(np.nonzero(l2[:-1] > 0)[0][-1])
+        take = min(int(l2[j]), -int(l2[-1]))
+        l2[j] -= take
+        l2[-1] += take
+    lens = np.concatenate([l1, np.zeros(5, dtype=l1.dtype), l2]).astype(np.uint64)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(lens, out=off[1:])
+    data = oracle.gen_bytes(int(off[-1]), byte_off=12345)
+    return off, data
+
+
 def _worker(rank, world, port, n, key_len, q, mode="cpu"):
     """mode: "cpu" (scalar plugin hashes, counts given), "auto" (counts exchanged by
     gather_hashes itself), "subgroup" (gather inside the group of global ranks 1..world-1
@@ -65,6 +93,23 @@ def _worker(rank, world, port, n, key_len, q, mode="cpu"):
         sys.path.insert(0, str(root / "oracle"))
         import k2hash_amd
         import oracle
+        if mode in ("csr_cpu", "csr_gpu"):  # one CSR batch cut by bytes, each shard rebased
+            off, data = _csr_batch(world, n)
+            cuts = shard.csr_cuts(off, world)
+            first, last = cuts[rank]
+            loc = shard.rebase_offsets(off, first, last)
+            mine = data[int(off[first]):int(off[last])]
+            if mode == "csr_gpu":
+                h, _ = k2hash_amd.hash_csr(torch.from_numpy(mine.copy()).to("cuda:0"),
+                                           torch.from_numpy(loc.astype(np.int64)).to("cuda:0"))
+                torch.cuda.synchronize()
+            else:
+                h = torch.tensor([k2hash_amd.k2h_hash(mine[int(loc[i]):int(loc[i + 1])].tobytes())
+                                  for i in range(last - first)], dtype=torch.uint64).view(torch.int64)
+            out = shard.gather_hashes(h, dst=0, counts=[b - a for a, b in cuts])
+            if rank == 0:
+                q.put(("csr", cuts, out.cpu().numpy().copy()))
+            return
         first, last = shard.shard_range(n, rank, world)
         data = oracle.gen_bytes((last - first) * key_len, byte_off=first * key_len)
         if mode == "gpu":
@@ -139,3 +184,38 @@ def test_gather_hip_hashes(oracle):
     gathered = [r for r in results if not isinstance(r, tuple)][0]
     assert np.array_equal(np.asarray(gathered).view(np.uint64), ref)
     assert all(np.array_equal(r[1].view(np.uint64), ref) for r in results if isinstance(r, tuple))
+
+
+def _check_csr(world, mode):
+    import sys
+    from pathlib import Path
+    sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "oracle"))
+    import oracle
+    n = 30011
+    (tag, cuts, got), = _run(world, n, 0, mode, 1)
+    off, data = _csr_batch(world, n)
+    ref, _ = oracle.hash_csr(data, off)
+    assert tag == "csr" and [tuple(c) for c in cuts] == shard.csr_cuts(off, world)
+    assert np.array_equal(got.view(np.uint64), ref)
+    lens = np.diff(off.astype(np.int64))
+    if world == 2:  # the cut falls on the run of zero-length keys, which rank 1 starts with
+        c = cuts[1][0]
+        assert lens[c] == 0 and lens[c - 1] > 0 and (ref[c:c + 5] == 0).all()
+    nbytes = [int(off[b]) - int(off[a]) for a, b in cuts]
+    assert max(nbytes) - min(nbytes) <= 2 * 300
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_csr_shards_by_bytes_gathered(world):
+    """One CSR batch cut by bytes (shard_csr_by_bytes), each shard's offsets rebased, each
+    rank hashing only its own bytes (scalar plugin), gathered to rank 0 with the per-rank
+    counts: bit-for-bit the oracle's hashes of the whole batch (SURVEY 8e)."""
+    _check_csr(world, "csr_cpu")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_csr_shards_by_bytes_hip_gathered(world):
+    """The same with each rank's shard hashed by the HIP CSR kernel on cuda:0 (ranks share
+    the card over gloo), a zero-length key run on the world-2 cut (VERDICT r3 #2)."""
+    _check_csr(world, "csr_gpu")
