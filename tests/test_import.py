@@ -290,8 +290,10 @@ def test_device_scan_over_4gib_tile_scan_runs(cuda):
 
 @pytest.mark.gpu
 def test_fused_scan_prehash_concurrent_threads(cuda, oracle):
-    """Calls from several host threads at once (the per-device scratch and the mapped record
-    count are shared under a lock): every call returns its own file's records and hashes."""
+    """Calls from several host threads at once, each on its own stream (the per-device
+    scratch and the mapped record count are shared under a lock, so each call must finish
+    its own stream's work before it releases them -- ADVICE r3): every call returns its own
+    file's records and hashes."""
     import concurrent.futures
     import torch
 
@@ -309,17 +311,24 @@ def test_fused_scan_prehash_concurrent_threads(cuda, oracle):
 
     def work(k):
         data, host, (hh1, hh2) = files[k]
-        f = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda)
-        for _ in range(5):
-            recs, h1, h2 = archive.import_scan_prehash_device(f, "tsv")
-            torch.cuda.synchronize()
-            a = recs.cpu().numpy().view(np.uint64)
-            assert a.shape[0] == host.size
-            for i, name in enumerate(archive.IMPORT_DTYPE.names):
-                assert np.array_equal(a[:, i], host[name])
-            assert np.array_equal(h1.cpu().numpy().view(np.uint64), hh1)
-            assert np.array_equal(h2.cpu().numpy().view(np.uint64), hh2)
+        s = torch.cuda.Stream(device=cuda)
+        with torch.cuda.stream(s):  # the file, the outputs and the call all on this thread's stream
+            f = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda, non_blocking=False)
+            for _ in range(5):
+                recs, h1, h2 = archive.import_scan_prehash_device(f, "tsv", stream=s)
+                s.synchronize()
+                out = (recs.cpu(), h1.cpu(), h2.cpu())
+                _check(out, host, hh1, hh2)
         return True
+
+    def _check(out, host, hh1, hh2):
+        recs, h1, h2 = out
+        a = recs.numpy().view(np.uint64)
+        assert a.shape[0] == host.size
+        for i, name in enumerate(archive.IMPORT_DTYPE.names):
+            assert np.array_equal(a[:, i], host[name])
+        assert np.array_equal(h1.numpy().view(np.uint64), hh1)
+        assert np.array_equal(h2.numpy().view(np.uint64), hh2)
 
     with concurrent.futures.ThreadPoolExecutor(4) as ex:
         assert all(ex.map(work, range(4)))
