@@ -1,20 +1,18 @@
 // k2hash_amd -- k2himport input scan on the GPU.
 //
 // The same records as the host scanner (k2h_import.cc, restating the std::getline loops
-// of tests/k2himport.cc:74-117) for a file that already sits in HBM, without a host pass:
-//
-// TSV (ConvertfromTsv, tests/k2himport.cc:74-89): the getline loop run as its own
-// two-mode machine, scanned over the bytes (see "TSV as the getline loop's own machine"
-// below): two streaming reads of the file, 32 B per record written, keys hashed from LDS.
-// mdbm (ConvertfromMdbm, tests/k2himport.cc:95-117).  Five header lines (the fifth
-// "HEADER=END", checked on the host from the first newline positions), then line
-// pairs; the EOF rules of the host scanner (an empty value after a key line that ends
-// the file with '\n', the previous record's value after a key line that ends at EOF).
-// Lines are found by two passes over 16 KiB blocks: (1) per block, its newline count and
-// whether a NUL follows its last newline, scanned across blocks; (2) every newline's
-// position and every line's first NUL (the C-string cut), written directly, each thread
-// knowing from the scanned state whether a NUL is its line's first.  Outputs: 16 B per
-// line plus 32 B per record.
+// of tests/k2himport.cc:74-117) for a file that already sits in HBM, without a host pass.
+// Both formats are one two-mode machine, scanned over the bytes (see "TSV as the getline
+// loop's own machine" below): the file read once, 32 B per record written, one
+// synchronisation per call.
+// TSV (ConvertfromTsv, tests/k2himport.cc:74-89): mode K reads a key up to its TAB, mode V
+// a value up to its newline; keys hashed from LDS by pass A.
+// mdbm (ConvertfromMdbm, tests/k2himport.cc:95-117): key lines and value lines alternate;
+// the five header lines are the machine's first records (the fifth, "HEADER=END", checked
+// where it ends); the EOF rules of the host scanner (an empty value after a key line that
+// ends the file with '\n', the previous record's value after a key line that ends at EOF).
+// Round 4: mdbm moved onto the TSV machinery (round 1-3: newline-position and line arrays,
+// hipcub device scans, three synchronisations and seven per-call pool allocations).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <stdint.h>
@@ -30,140 +28,6 @@ namespace k2h {
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kBytesPerThread = 64;
-constexpr uint64_t kChunk = (uint64_t)kThreads * kBytesPerThread;  // 16 KiB per block
-constexpr uint64_t kNone = ~0ull;
-
-// Exact per-byte "equals c" mask of a 32-bit word: bit 7 of each matching byte.
-__device__ inline uint32_t eq_mask(uint32_t w, uint32_t c4) {
-  uint32_t v = w ^ c4;
-  uint32_t t = (v & 0x7F7F7F7Fu) + 0x7F7F7F7Fu;
-  return ~(t | v | 0x7F7F7F7Fu);
-}
-
-// Bytes [b, e) of this thread's 64-byte span, as 16 words with out-of-range bytes
-// replaced by a non-newline value; aligned fast path when the span is whole.
-__device__ inline void load_span(const uint8_t* f, uint64_t size, uint64_t b, uint32_t w[16]) {
-  if (b + 64 <= size && (((uintptr_t)(f + b)) & 15) == 0) {
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4* p = reinterpret_cast<const u32x4*>(f + b);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      u32x4 v = __builtin_nontemporal_load(p + q);
-      w[4 * q] = v.x, w[4 * q + 1] = v.y, w[4 * q + 2] = v.z, w[4 * q + 3] = v.w;
-    }
-    return;
-  }
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    uint32_t x = 0x01010101u;
-    for (int j = 0; j < 4; ++j) {
-      uint64_t i = b + 4 * k + j;
-      if (i < size) x = (x & ~(0xFFu << (8 * j))) | ((uint32_t)f[i] << (8 * j));
-    }
-    w[k] = x;
-  }
-}
-
-__device__ inline uint64_t line_begin(const uint64_t* nl, uint64_t j) { return j ? nl[j - 1] + 1 : 0; }
-__device__ inline uint64_t line_end(const uint64_t* nl, uint64_t nnl, uint64_t size, uint64_t j) {
-  return j < nnl ? nl[j] : size;
-}
-
-// State of the line open at some point of the file, summarised over a span of bytes:
-// whether the span holds a newline, and whether a NUL was seen since its last newline
-// (or its start).  Combining spans in file order is associative (a segmented "or"), so
-// blocks and threads get their incoming state from scans.
-enum : uint32_t { kHasNl = 1, kNul = 2 };
-struct SpanOp {
-  __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const {
-    if (b & kHasNl) return b;
-    return (a & kHasNl) | ((a | b) & kNul);
-  }
-};
-
-struct CountStateOp {  // (newline count << 8 | span state) pairs, combined in file order
-  __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const {
-    return (((a >> 8) + (b >> 8)) << 8) | SpanOp()(a & 0xFFu, b & 0xFFu);
-  }
-};
-
-__device__ inline uint32_t nl_count(const uint32_t w[16]) {
-  uint32_t c = 0;
-#pragma unroll
-  for (int k = 0; k < 16; ++k) c += __popc(eq_mask(w[k], 0x0A0A0A0Au));
-  return c;
-}
-
-// Walk the span's newlines and NULs in byte order from state `st`; with Write, record
-// each newline position and each line's first NUL.  Returns the state after the span.
-template <bool Write>
-__device__ inline uint32_t span_walk(const uint32_t w[16], uint64_t b, uint32_t st, uint64_t line,
-                                     uint64_t* __restrict__ nl, uint64_t* __restrict__ lnul) {
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const uint32_t mnl = eq_mask(w[k], 0x0A0A0A0Au);
-    uint32_t x = mnl | eq_mask(w[k], 0);
-    while (x) {
-      const int bit = __builtin_ctz(x);
-      x &= x - 1;
-      const uint64_t pos = b + 4 * k + (bit >> 3);
-      if (mnl & (1u << bit)) {
-        if constexpr (Write) nl[line] = pos;
-        ++line;
-        st = kHasNl;
-      } else if (!(st & kNul)) {
-        if constexpr (Write) lnul[line] = pos;
-        st |= kNul;
-      }
-    }
-  }
-  return st;
-}
-
-// Pass 1: per block, the newline count and the span state.
-__global__ __launch_bounds__(kThreads) void span_count_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                              uint64_t* __restrict__ block_cnt,
-                                                              uint32_t* __restrict__ block_state) {
-  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
-  uint32_t c = 0, st = 0;
-  if (b < size) {
-    uint32_t w[16];
-    load_span(f, size, b, w);
-    c = nl_count(w);
-    st = span_walk<false>(w, b, 0, 0, nullptr, nullptr);
-  }
-  typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
-  __shared__ typename Scan::TempStorage tmp;
-  uint32_t inc;
-  Scan(tmp).InclusiveScan((c << 8) | st, inc, CountStateOp());  // <= 2^14 newlines per block
-  if (threadIdx.x == kThreads - 1) {
-    block_cnt[blockIdx.x] = inc >> 8;
-    block_state[blockIdx.x] = inc & 0xFFu;
-  }
-}
-
-// Pass 2 (block_base / block_in = exclusive scans of pass 1): newline positions in order
-// and every line's first NUL.
-__global__ __launch_bounds__(kThreads) void span_write_kernel(const uint8_t* __restrict__ f, uint64_t size,
-                                                              const uint64_t* __restrict__ block_base,
-                                                              const uint32_t* __restrict__ block_in,
-                                                              uint64_t* __restrict__ nl, uint64_t* __restrict__ lnul) {
-  const uint64_t b = (uint64_t)blockIdx.x * kChunk + (uint64_t)threadIdx.x * kBytesPerThread;
-  uint32_t w[16];
-  uint32_t c = 0, st = 0;
-  if (b < size) {
-    load_span(f, size, b, w);
-    c = nl_count(w);
-    st = span_walk<false>(w, b, 0, 0, nullptr, nullptr);
-  }
-  typedef hipcub::BlockScan<uint32_t, kThreads> Scan;
-  __shared__ typename Scan::TempStorage tmp;
-  uint32_t co;
-  Scan(tmp).ExclusiveScan((c << 8) | st, co, block_in[blockIdx.x], CountStateOp());
-  if (b >= size) return;
-  span_walk<true>(w, b, co & 0xFFu, block_base[blockIdx.x] + (co >> 8), nl, lnul);
-}
 
 // One lane per record: the key straight from the file (no gather) as k = ceil(len/16)
 // 16-byte chunks that END at its last byte (the CSR kernels' end-aligned form): chunk 0
@@ -219,48 +83,6 @@ __global__ __launch_bounds__(kThreads) void import_hash_kernel(const uint8_t* __
   if (off <= size && len <= size - off) hash_cstr(f, off, len, sp, a, b);  // else: never read past the file
   h1[i] = a;
   if (h2) h2[i] = b;
-}
-
-// mdbm: key line 5 + 2r, value line 6 + 2r (see the header comment for the EOF rules).
-__global__ __launch_bounds__(kThreads) void mdbm_records_kernel(const uint64_t* __restrict__ nl, uint64_t nnl,
-                                                                uint64_t size, const uint64_t* __restrict__ lnul,
-                                                                uint64_t nlines, uint64_t nrec, uint64_t body,
-                                                                k2h_amd_import_rec* __restrict__ recs,
-                                                                const uint8_t* __restrict__ f, SpadTable sp,
-                                                                uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
-  const uint64_t r = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
-  if (r >= nrec) return;
-  const uint64_t kl = 5 + 2 * r;
-  auto cut = [&](uint64_t j) {  // strlen of line j's C string
-    const uint64_t b = line_begin(nl, j), e = line_end(nl, nnl, size, j);
-    return (lnul[j] != kNone ? lnul[j] : e) - b;
-  };
-  k2h_amd_import_rec o;
-  o.key_off = line_begin(nl, kl);
-  o.key_len = cut(kl);
-  if (kl < nnl) {  // key line ends in '\n'
-    const uint64_t vl = kl + 1;
-    if (vl < nlines) {
-      o.val_off = line_begin(nl, vl);
-      o.val_len = cut(vl);
-    } else {  // the file ends after the key line: the value getline fails
-      o.val_off = size;
-      o.val_len = 0;
-    }
-  } else if (r) {  // key line at EOF: the previous record's value (getline kept it)
-    o.val_off = line_begin(nl, kl - 1);
-    o.val_len = cut(kl - 1);
-  } else {
-    o.val_off = body;
-    o.val_len = 0;
-  }
-  recs[r] = o;
-  if (h1) {  // fused prehash: the key as the C string Set stores
-    uint64_t a, b;
-    hash_cstr(f, o.key_off, o.key_len, sp, a, b);
-    h1[r] = a;
-    if (h2) h2[r] = b;
-  }
 }
 
 unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
@@ -446,8 +268,12 @@ constexpr uint32_t kEvCap = 5;
 constexpr uint64_t kNoSlots = 0xFFFFull << 48;
 constexpr uint64_t kEvOverflow = (7ull << 45) | kNoSlots;
 __device__ inline uint32_t ev_count(uint64_t pk) { return (uint32_t)(pk >> 45) & 7u; }
-// 0x0A -> 1, 0x09 -> 2, 0x00 -> 3, other bytes 0: two bits per byte value below 11
-__device__ inline uint32_t ev_type(uint32_t c) { return c < 11u ? (0x180003u >> (2 * c)) & 3u : 0u; }
+// 0x0A -> 1, 0x09 -> 2 (TSV only: a TAB is an ordinary byte of an mdbm line), 0x00 -> 3,
+// other bytes 0: two bits per byte value below 11
+template <bool MDBM>
+__device__ inline uint32_t ev_type(uint32_t c) {
+  return c < 11u ? ((MDBM ? 0x100003u : 0x180003u) >> (2 * c)) & 3u : 0u;
+}
 
 // The function of one event at position p1 (block-relative + 1), composed onto a span's
 // accumulated function without branches (round 3; the per-type branches cost ~50 SALU and
@@ -456,22 +282,30 @@ __device__ inline uint32_t ev_type(uint32_t c) { return c < 11u ? (0x180003u >> 
 //            one record end, boundary p1);
 //   TAB:     entered in K, the key ends (exit V, boundary p1); entered in V, part of the value;
 //   NUL:     the last NUL; any other byte (type 0): the identity.
+// mdbm (ConvertfromMdbm, tests/k2himport.cc:107-112) is the same machine with lines for
+// fields: a key line and a value line alternate, so a newline entered in K ends the key
+// (exit V, boundary p1) and entered in V ends the record (exit K, one record end, boundary
+// p1); TABs are ordinary bytes.
+template <bool MDBM>
 __device__ inline LFn ev_fn(uint32_t t, uint32_t p1) {
   const bool nl = t == 1u, tab = t == 2u;
+  if constexpr (MDBM)
+    return LFn{nl ? (kSelV | (kSelK << 16)) : (kSelK | (kSelV << 16)), nl ? 0x10000u : 0u,
+               nl ? p1 | (p1 << 16) : 0u, t == 3u ? p1 : 0u};
   return LFn{nl ? (kSelK | (kSelK << 16)) : tab ? (kSelV | (kSelV << 16)) : (kSelK | (kSelV << 16)),
              nl ? 0x10000u : 0u, nl ? p1 << 16 : tab ? p1 : 0u, t == 3u ? p1 : 0u};
 }
 
 // Walk the candidate bytes of a span staged at `span`, calling f(offset, type) for each
 // (type 0 for a candidate that is no event: f must treat it as none).
-template <class F>
+template <bool MDBM, class F>
 __device__ inline void span_events(const uint8_t* span, F&& f) {
   uint64_t mm[2];
   tsv_events(span, mm[0], mm[1]);
   uint32_t o = next_event(mm[0], mm[1]), c = span[o & 127u];
   while (o < 128) {
     const uint32_t on = next_event(mm[0], mm[1]), cn = span[on & 127u];
-    f(o, ev_type(c));
+    f(o, ev_type<MDBM>(c));
     o = on;
     c = cn;
   }
@@ -508,6 +342,14 @@ __device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, con
 // is in an earlier block, a third cut in one span, a span with more than kEvCap events)
 // is hashed from the file.
 constexpr uint32_t kSlots = 2;
+// The head key: the key that ends at a block's first cut event when no newline precedes it
+// in the block started in the bytes before the block (a key straddling the boundary, ~1 in
+// 4 blocks on BASELINE-like files).  Pass A stages kPre bytes before the block too and
+// hashes it from the byte after the last newline among them (start < 0, block-relative);
+// before round 4 pass B hashed every such key from the file, one lane holding its wave
+// (~47 us of a 0.62 ms call, profiles/r04d_import_probes.txt).  Block 0's head key starts
+// at the file's first byte.
+constexpr uint32_t kPre = 256;
 constexpr uint32_t kListCap = 160;  // keys hashed by pass A per block (BASELINE-like files: ~120; < 0xFF)
 // A block's list is two arrays at the same index: the FNV state after the key's bytes (h2
 // of key + NUL; h1 = raw * P) and the key's block-relative start (10 bytes per key).
@@ -567,7 +409,14 @@ struct EntryScan {
   uint64_t* count;     // records in the file
   uint64_t* host_count;  // the same, into mapped pinned host memory (no read-back copy)
   uint64_t nblk, ntile;
+  uint64_t size;
+  uint32_t mdbm;  // the mdbm machine: starts in V (see kHdrRecs), counts a key line at EOF
 };
+// mdbm: the machine starts in mode V at the file's first byte, so the five header lines are
+// "records" 0 (its value line 0), 1 (lines 1-2) and 2 (lines 3-4), and the key line after
+// the header starts record kHdrRecs -- real record r is machine record r + kHdrRecs.  The
+// fifth header line is record 2's value line (checked in pass B).
+constexpr uint64_t kHdrRecs = 3;
 
 // Exclusive scan of in[0, n) by one block, thread t owning the run [t k, (t + 1) k):
 // out(i, prefix of in[0, i)); returns the whole reduction.  Runs of up to 4 are loaded
@@ -606,28 +455,49 @@ __device__ inline GFn block_scan_runs(Tmp& tmp, const GFn* in, uint64_t n, uint6
 }
 
 // Pass A: each block's function (for tsv_scan_kernel), each thread's packed events, and
-// the speculative key states.
+// the speculative key states (TSV only: which mdbm lines are keys depends on the line
+// count before the block, so pass B hashes mdbm keys from the file).
+template <bool MDBM>
 __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                           GFn* __restrict__ blk_fn, uint64_t* __restrict__ ev,
                                                           SpecList spec, SpadTable sp) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[16 + kTChunk];
-  __shared__ uint64_t s_key[kListCap];  // emitted keys: start | len << 16 | slot index << 32
+  constexpr uint32_t PRE = MDBM ? 0u : kPre;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[16 + PRE + kTChunk];
+  __shared__ uint64_t s_key[kListCap];  // emitted keys: start (16-bit, signed) | len << 16
   __shared__ uint32_t s_nk;
   typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
   __shared__ typename NlScan::TempStorage tmp;
   __shared__ LFn s_wave[kTThreads / 64];
   if (threadIdx.x == 0) s_nk = 0;
-  tsv_stage(f, size, blockIdx.x, lds);  // (its barrier publishes s_nk = 0)
-  const uint32_t rel = kTBytes * threadIdx.x;
-  const uint8_t* span = lds + 16 + rel;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
+  if (!MDBM && threadIdx.x < PRE / 16) {  // the kPre bytes before the block, for its head key
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 v = u32x4{0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};  // block 0: no event
+    if (base) {
+      const uint8_t* p = f + base - PRE + 16 * threadIdx.x;  // (base >= 16 KiB > PRE)
+      if ((((uintptr_t)p) & 15) == 0) {
+        v = *reinterpret_cast<const u32x4*>(p);
+      } else {
+        uint32_t x[4];
+        for (int k = 0; k < 4; ++k)
+          x[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+                 ((uint32_t)p[4 * k + 3] << 24);
+        v = u32x4{x[0], x[1], x[2], x[3]};
+      }
+    }
+    *reinterpret_cast<u32x4*>(lds + 16 + 16 * threadIdx.x) = v;
+  }
+  uint8_t* blk = lds + PRE;  // block byte i at blk[16 + i]; the prefix below it
+  tsv_stage(f, size, blockIdx.x, blk);  // (its barrier publishes s_nk = 0 and the prefix)
+  const uint32_t rel = kTBytes * threadIdx.x;
+  const uint8_t* span = blk + 16 + rel;
   const bool live = base + rel < size;
   LFn acc = lfn_id();
   uint64_t pk = 0;
   uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
   if (live)
-    span_events(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
-      acc = LCompose()(acc, ev_fn(t, rel + o + 1));
+    span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
+      acc = LCompose()(acc, ev_fn<MDBM>(t, rel + o + 1));
       const uint64_t e = (uint64_t)(o | (t << 7)) << (9 * min(ne, kEvCap - 1));
       pk |= (t && ne < kEvCap) ? e : 0ull;
       ne += t ? 1u : 0u;
@@ -635,31 +505,56 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     });
   const bool over = ne > kEvCap;
   pk = over ? kEvOverflow : pk | ((uint64_t)ne << 45) | kNoSlots;
-  uint32_t pre_nl;
-  NlScan(tmp).ExclusiveScan(live ? nl : 2u, pre_nl, 2u, NlOp());
   const LFn bf = block_fn_reduce(acc, s_wave);
   if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(bf, base);
+  if constexpr (MDBM) {
+    ev[base / kTBytes + threadIdx.x] = pk;
+    return;
+  }
+  uint32_t pre_nl;
+  NlScan(tmp).ExclusiveScan(live ? nl : 2u, pre_nl, 2u, NlOp());
   // keys ending at this span's cuts: the newline state entering the span, then its events;
-  // each key goes to the block's list, hashed below one lane per key
-  bool open = (pre_nl & 3u) == 3u;
-  uint32_t start = (pre_nl >> 2) + 1, j = 0;
+  // each key goes to the block's list, hashed below one lane per key.  head: no newline and
+  // no cut before this span in the block, so its first cut may end the head key.
+  bool open = (pre_nl & 3u) == 3u, head = pre_nl == 2u;
+  int32_t start = (int32_t)(pre_nl >> 2) + 1;
+  uint32_t j = 0;
   if (live && !over) {
     for (uint32_t q = 0; q < ne; ++q) {
       const uint32_t e = (uint32_t)(pk >> (9 * q)) & 0x1FFu;
       const uint32_t pos = rel + (e & 127u), t = e >> 7;
       if (t == 1u) {
         open = true;
-        start = pos + 1;
+        head = false;
+        start = (int32_t)pos + 1;
         continue;
       }
-      if (open && j < kSlots && base + pos < size) {  // the first cut after a newline of this block
-        const uint32_t slot = atomicAdd(&s_nk, 1u);
+      if ((open || head) && j < kSlots && base + pos < size) {  // the first cut after a newline
+        bool ok = true;
+        if (head) {  // the byte after the last newline of the prefix (block 0: the file's first)
+          ok = base == 0;
+          start = 0;
+          for (int32_t w = (int32_t)PRE / 16 - 1; w >= 0 && !ok; --w) {
+            const uint4 c = ld16(lds + 16 + 16 * w);
+            const uint32_t wd[4] = {c.x, c.y, c.z, c.w};
+            for (int32_t k = 3; k >= 0 && !ok; --k) {
+              const uint32_t x = wd[k] ^ 0x0A0A0A0Au;
+              const uint32_t m = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // bit 7 of 0x0A bytes
+              if (m) {
+                start = 16 * w + 4 * k + (31 - (int32_t)__clz(m)) / 8 + 1 - (int32_t)PRE;
+                ok = true;
+              }
+            }
+          }
+        }
+        const uint32_t slot = ok ? atomicAdd(&s_nk, 1u) : kListCap;
         if (slot < kListCap) {
-          s_key[slot] = start | ((uint64_t)(pos - start) << 16);
+          s_key[slot] = ((uint32_t)start & 0xFFFFu) | ((uint64_t)((int32_t)pos - start) << 16);
           pk = (pk & ~(0xFFull << (48 + 8 * j))) | ((uint64_t)slot << (48 + 8 * j));
         }
       }
       open = false;
+      head = false;
       ++j;
     }
   }
@@ -668,9 +563,10 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   const uint32_t nk = min(s_nk, kListCap);
   for (uint32_t i = threadIdx.x; i < nk; i += kTThreads) {
     const uint64_t k = s_key[i];
-    const uint32_t st = (uint32_t)k & 0xFFFFu, len = (uint32_t)(k >> 16) & 0xFFFFu;
-    spec.raw[(uint64_t)blockIdx.x * kListCap + i] = key_raw_lds(lds + 16 + st, len, sp);
-    spec.start[(uint64_t)blockIdx.x * kListCap + i] = (uint16_t)st;
+    const int32_t st = (int16_t)(k & 0xFFFFu);
+    const uint32_t len = (uint32_t)(k >> 16) & 0xFFFFu;
+    spec.raw[(uint64_t)blockIdx.x * kListCap + i] = key_raw_lds(blk + 16 + st, len, sp);
+    spec.start[(uint64_t)blockIdx.x * kListCap + i] = (uint16_t)(k & 0xFFFFu);
   }
 }
 
@@ -695,13 +591,20 @@ __global__ __launch_bounds__(kTThreads) void tsv_scan_kernel(EntryScan es) {
   if (!s_last) return;
   __threadfence();  // acquire: every tile's function
   const uint64_t k = (es.ntile + kTThreads - 1) / kTThreads;
-  const TState s0{0, 0, 0, 0};
+  const TState s0{es.mdbm, 0, 0, 0};
   const GFn all = block_scan_runs(gtmp, es.tile_fn, es.ntile, k,
                                   [&](uint64_t i, const GFn& p) { es.tile_in[i] = gapply(p, s0); });
   if (threadIdx.x == 0) {
     const TState e = gapply(all, s0);
-    es.count[0] = e.r + e.m;
-    __hip_atomic_store(es.host_count, e.r + e.m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    // a value getline at EOF ends one more record; mdbm: so does a key line that ends at EOF
+    // with bytes in it (tests/k2himport.cc:107-112: the key getline extracts them)
+    uint64_t n = e.r + e.m;
+    if (es.mdbm) {
+      n += (!e.m && e.fs < es.size) ? 1u : 0u;
+      n = n > kHdrRecs ? n - kHdrRecs : 0u;
+    }
+    es.count[0] = n;
+    __hip_atomic_store(es.host_count, n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     es.done[0] = 0;
   }
 }
@@ -711,7 +614,12 @@ __global__ __launch_bounds__(kTThreads) void tsv_scan_kernel(EntryScan es) {
 // prefixes stored), the walk, the records, and every key's h1 / h2 -- pass A's state when
 // its slot matches the key, else hashed from the file.  Fields are written only for
 // records below min(count, cap), so a key cut off by EOF writes nothing.
-template <bool HASH>
+// mdbm (MDBM): records are machine records - kHdrRecs; the thread that ends machine record
+// 2's value line checks the fifth header line ("HEADER=END", tests/k2himport.cc:101-104)
+// and sets hflags[1]; a last key line that ends at EOF takes the previous record's value
+// (getline leaves the string as it was when it fails at EOF) -- the first record's
+// directly, any later one by the host after the call (hflags[2], a 16-byte copy).
+template <bool HASH, bool MDBM>
 __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                           const GFn* __restrict__ intile,
                                                           const TState* __restrict__ tile_in,
@@ -720,9 +628,11 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
                                                           const uint16_t* __restrict__ spec_start,
                                                           const uint64_t* __restrict__ count, uint64_t cap,
                                                           k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
-                                                          uint64_t* __restrict__ h1, uint64_t* __restrict__ h2) {
+                                                          uint64_t* __restrict__ h1, uint64_t* __restrict__ h2,
+                                                          uint64_t* __restrict__ hflags) {
   typedef hipcub::BlockScan<LFn, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> Scan;
   __shared__ typename Scan::TempStorage tmp;
+  constexpr uint64_t HDR = MDBM ? kHdrRecs : 0;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
   const uint32_t rel = kTBytes * threadIdx.x;
   const bool live = base + rel < size;
@@ -739,7 +649,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
     sl_raw[j] = 0;
     sl_start[j] = 0xFFFFFFFFu;
     const uint32_t li = (uint32_t)(pk >> (48 + 8 * j)) & 0xFFu;
-    if (HASH && li != 0xFFu) {
+    if (HASH && !MDBM && li != 0xFFu) {
       sl_raw[j] = spec_raw[(uint64_t)blockIdx.x * kListCap + li];
       sl_start[j] = spec_start[(uint64_t)blockIdx.x * kListCap + li];
     }
@@ -780,7 +690,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
     if (over) {
       uint64_t m0 = om0, m1 = om1;
       for (uint32_t o = next_event(m0, m1); o < 128 && base + rel + o < size; o = next_event(m0, m1)) {
-        const uint32_t t = ev_type(f[base + rel + o]);  // (bytes past the file are 0x01 in the masks)
+        const uint32_t t = ev_type<MDBM>(f[base + rel + o]);  // (bytes past the file are 0x01 in the masks)
         if (t) fn(o, t);
       }
     } else {
@@ -792,11 +702,11 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
     }
   };
   LFn acc = lfn_id();
-  for_events([&](uint32_t o, uint32_t t) { acc = LCompose()(acc, ev_fn(t, rel + o + 1)); });
+  for_events([&](uint32_t o, uint32_t t) { acc = LCompose()(acc, ev_fn<MDBM>(t, rel + o + 1)); });
   LFn pre;
   Scan(tmp).ExclusiveScan(acc, pre, lfn_id(), LCompose());
   TState s = gapply(gfn_of(pre, base), gapply(ein, tin));
-  const uint64_t lim = min(count[0], cap);
+  const uint64_t lim = min(count[0], cap) + HDR;  // machine record indices below lim are written
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
   uint32_t j = 0;           // cut events of this span so far
   // a key ended in this span whose record's value has not ended yet: its fields wait so
@@ -808,14 +718,17 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
     pk_r = ~0ull;
   };
   auto key_end = [&](uint64_t e) {
-    if (s.r >= lim) return;
+    if (s.r < HDR || s.r >= lim) return;
+    const uint64_t r = s.r - HDR;
     flush_key();
-    pk_r = s.r;
+    pk_r = r;
     pk_off = s.fs;
     pk_len = e - s.fs;
     if constexpr (HASH) {
       uint64_t a, c;
-      const uint32_t want = s.fs >= base ? (uint32_t)(s.fs - base) : 0xFFFFFFFEu;
+      // the key's start relative to the block as pass A stored it (16 bits; a key that
+      // starts in the bytes before the block, pass A's head key, is negative)
+      const uint32_t want = s.fs + kTChunk >= base ? (uint32_t)((s.fs - base) & 0xFFFFu) : 0xFFFFFFFEu;
       bool hit = false;
       uint64_t raw = 0;
 #pragma unroll
@@ -830,27 +743,41 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
       } else {
         hash_cstr(f, s.fs, e - s.fs, sp, a, c);
       }
-      h1[s.r] = a;
-      if (h2) h2[s.r] = c;
+      h1[r] = a;
+      if (h2) h2[r] = c;
     }
   };
-  auto val_end = [&](uint64_t e) {
-    if (s.r >= lim) return;
-    if (pk_r == s.r) {
-      *reinterpret_cast<u64x2*>(&recs[s.r].key_off) = u64x2{pk_off, pk_len};
-      *reinterpret_cast<u64x2*>(&recs[s.r].val_off) = u64x2{s.fs, e - s.fs};
+  auto val_end = [&](uint64_t e, bool at_nul) {
+    if constexpr (MDBM) {
+      if (s.r == 2) {  // the fifth header line, compared whole (a NUL in it is a mismatch)
+        static constexpr char kEnd[] = "HEADER=END";
+        bool ok = !at_nul && e - s.fs == sizeof kEnd - 1;
+        for (uint32_t i = 0; ok && i < sizeof kEnd - 1; ++i) ok = f[s.fs + i] == (uint8_t)kEnd[i];
+        if (ok) __hip_atomic_store(hflags + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+    }
+    if (s.r < HDR || s.r >= lim) return;
+    const uint64_t r = s.r - HDR;
+    if (pk_r == r) {
+      *reinterpret_cast<u64x2*>(&recs[r].key_off) = u64x2{pk_off, pk_len};
+      *reinterpret_cast<u64x2*>(&recs[r].val_off) = u64x2{s.fs, e - s.fs};
       pk_r = ~0ull;
     } else {
-      *reinterpret_cast<u64x2*>(&recs[s.r].val_off) = u64x2{s.fs, e - s.fs};
+      *reinterpret_cast<u64x2*>(&recs[r].val_off) = u64x2{s.fs, e - s.fs};
     }
   };
   for_events([&](uint32_t o, uint32_t t) {
     const uint64_t pos = base + rel + o;
     if (t == 1u) {
       if (s.m) {  // the value getline's newline: the record ends
-        if (!nulf) val_end(pos);
+        if (!nulf) val_end(pos, false);
         s.m = 0;
         ++s.r;
+        s.fs = pos + 1;
+        nulf = false;
+      } else if (MDBM) {  // mdbm: the key line's newline
+        if (!nulf) key_end(pos);
+        s.m = 1;
         s.fs = pos + 1;
         nulf = false;
       }
@@ -864,80 +791,61 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
         nulf = false;
       }
     } else if (!nulf) {  // the field's first NUL: its C string ends here
-      if (s.m) val_end(pos);
+      if (s.m) val_end(pos, true);
       else key_end(pos);
       nulf = true;
     }
     ++j;
   });
-  // the thread holding the last byte: a value read to EOF
-  if (live && base + rel + kTBytes >= size && s.m && !nulf) val_end(size);
+  if (live && base + rel + kTBytes >= size) {  // the thread holding the last byte
+    if (s.m && !nulf) val_end(size, false);    // a value read to EOF
+    if constexpr (MDBM) {
+      if (!s.m && s.fs < size) {  // a key line at EOF: the key, and the previous record's value
+        if (!nulf) key_end(size);
+        if (s.r >= HDR && s.r < lim) {
+          if (s.r == HDR)
+            *reinterpret_cast<u64x2*>(&recs[0].val_off) = u64x2{s.fs, 0ull};
+          else
+            __hip_atomic_store(hflags + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      }
+    }
+  }
   flush_key();
 }
 
 }  // namespace
 
-__global__ void scan_summary_kernel(const uint8_t* __restrict__ f, uint64_t size, const uint64_t* __restrict__ bbase,
-                                    uint64_t nblk, uint64_t* __restrict__ out) {
-  out[0] = bbase[nblk];
-  out[1] = f[size - 1];
-}
-
-// Scratch for the per-call temporaries: a library-private stream-ordered pool per device
-// whose release threshold keeps up to kScratchKeep bytes of freed memory mapped (the
-// default pool returns everything at every synchronisation, so each call would map its
-// line / record arrays again).  Above the threshold, freed memory goes back to the device
-// at the next synchronisation, so a call over a huge file does not pin its peak for the
-// life of the process.
-constexpr uint64_t kScratchKeep = 512ull << 20;  // > the temporaries of a 1.2 GB TSV file (~23 % of its size)
-
-hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
-  constexpr int kMaxDev = 64;
-  static hipMemPool_t pools[kMaxDev] = {};
-  static std::once_flag once[kMaxDev];
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e != hipSuccess) return e;
-  if (dev < 0 || dev >= kMaxDev) return hipMallocAsync(p, bytes, stream);
-  std::call_once(once[dev], [dev] {
-    hipMemPoolProps props = {};
-    props.allocType = hipMemAllocationTypePinned;
-    props.handleTypes = hipMemHandleTypeNone;
-    props.location.type = hipMemLocationTypeDevice;
-    props.location.id = dev;
-    hipMemPool_t pool = nullptr;
-    if (hipMemPoolCreate(&pool, &props) != hipSuccess) return;
-    uint64_t keep = kScratchKeep;
-    (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
-    pools[dev] = pool;
-  });
-  return pools[dev] ? hipMallocFromPoolAsync(p, bytes, pools[dev], stream) : hipMallocAsync(p, bytes, stream);
-}
-
-// The TSV temporaries, one grow-only buffer per device held across calls (under a
+// The scan's temporaries, one grow-only buffer per device held across calls (under a
 // per-device lock for the call) while it stays within kScratchKeep: per-call pool
 // allocations of this size cost ~0.15 ms per hipFreeAsync on MI355X (rocprofv3
-// --runtime-trace, profiles/r03f_import_api_stats.csv), more than the scan itself.
+// --runtime-trace, profiles/r03f_import_api_stats.csv), more than the scan itself.  Above
+// kScratchKeep (a file of several GB) the buffer is freed at the end of the call, so a huge
+// file does not pin its peak for the life of the process.
 // The entry-state scan's counter lives in a second buffer that is never freed: it must be
 // zero at every call (the scan leaves it zero), so it is cleared only when allocated.
-struct TsvScratch {
+// The record count and the mdbm flags come back through mapped pinned host memory.
+constexpr uint64_t kScratchKeep = 512ull << 20;  // > the temporaries of a 1.2 GB TSV file (~23 % of its size)
+struct ScanScratch {
   std::mutex mu;
   void* p = nullptr;
   size_t bytes = 0;
-  void* cnt = nullptr;  // done (u32) at 0, count (u64) at 8
-  uint64_t* hcnt = nullptr;   // record count, mapped pinned host memory ...
-  uint64_t* hcnt_d = nullptr;  // ... and its device address
+  void* cnt = nullptr;      // done (u32) at 0, count (u64) at 8
+  uint64_t* hflags = nullptr;    // mapped pinned host memory: [0] count, [1] mdbm header ok, [2] mdbm fixup
+  uint64_t* hflags_d = nullptr;  // ... and its device address
 };
-TsvScratch g_tsv[64];
+ScanScratch g_scan[64];
 
 static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// TSV: pass A, the scan of block functions (and the count), pass B (when recs), one
-// read-back.  Temporaries per 16 KiB block: its function and in-tile prefix (2 x 48 B),
-// 8 B of events per 128 B span, and the block's list of speculative key states (10 B
-// each, up to kListCap); per tile of kTile blocks its function and entry state.
-static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
-                      hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
+// TSV and mdbm: pass A, the scan of block functions (and the count), pass B (mdbm always:
+// it checks the header; TSV when records are wanted), one synchronisation.  Temporaries per
+// 16 KiB block: its function and in-tile prefix (2 x 48 B), 8 B of events per 128 B span,
+// and the block's list of speculative key states (TSV: 10 B each, up to kListCap); per tile
+// of kTile blocks its function and entry state.
+template <bool MDBM>
+static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
+                       hipStream_t stream, hipError_t* herr, uint64_t* h1, uint64_t* h2, uint64_t seed) {
   const uint64_t nblk = (size + kTChunk - 1) / kTChunk;
   hipError_t e = nblk > 0x7FFFFFFFull ? hipErrorInvalidValue : hipSuccess;
   auto tr = [&](hipError_t x) {
@@ -953,9 +861,10 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   const uint64_t ntile = (nblk + kTile - 1) / kTile;
   const size_t o_fn = 0, o_in = o_fn + align256(nblk * sizeof(GFn)), o_tf = o_in + align256(nblk * sizeof(GFn));
   const size_t o_ti = o_tf + align256(ntile * sizeof(GFn)), o_ev = o_ti + align256(ntile * sizeof(TState));
-  const size_t o_spec = o_ev + align256(nblk * kTThreads * 8), o_start = o_spec + align256(nblk * kListCap * 8);
-  const size_t total = o_start + align256(nblk * kListCap * 2);
-  TsvScratch& sc = g_tsv[dev];
+  const size_t nspec = MDBM ? 0 : nblk * kListCap;
+  const size_t o_spec = o_ev + align256(nblk * kTThreads * 8), o_start = o_spec + align256(nspec * 8);
+  const size_t total = o_start + align256(nspec * 2);
+  ScanScratch& sc = g_scan[dev];
   std::lock_guard<std::mutex> lk(sc.mu);
   if (e == hipSuccess && sc.bytes < total) {
     if (sc.p) tr(hipFree(sc.p));
@@ -969,18 +878,24 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
     tr(hipMemsetAsync(sc.cnt, 0, 256, stream));
     if (e != hipSuccess) sc.cnt = nullptr;
   }
-  if (e == hipSuccess && !sc.hcnt) {  // the count comes back without a copy command
+  if (e == hipSuccess && !sc.hflags) {  // the count and flags come back without a copy command
     void* hp = nullptr;
     tr(hipHostMalloc(&hp, 64, hipHostMallocMapped));
     void* dp = nullptr;
     if (e == hipSuccess) tr(hipHostGetDevicePointer(&dp, hp, 0));
     if (e == hipSuccess) {
-      sc.hcnt = (uint64_t*)hp;
-      sc.hcnt_d = (uint64_t*)dp;
+      sc.hflags = (uint64_t*)hp;
+      sc.hflags_d = (uint64_t*)dp;
     } else if (hp) {
       (void)hipHostFree(hp);
     }
   }
+  if (e != hipSuccess) {
+    *herr = e;
+    return K2H_AMD_EHIP;
+  }
+  sc.hflags[1] = 0;  // the previous call on this device has synchronised (the lock)
+  sc.hflags[2] = 0;
   uint8_t* base = (uint8_t*)sc.p;
   uint8_t* cb = (uint8_t*)sc.cnt;
   EntryScan es;
@@ -990,34 +905,43 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   es.tile_in = (TState*)(base + o_ti);
   es.done = (uint32_t*)cb;
   es.count = (uint64_t*)(cb + 8);
-  es.host_count = sc.hcnt_d;
+  es.host_count = sc.hflags_d;
   es.nblk = nblk;
   es.ntile = ntile;
+  es.size = size;
+  es.mdbm = MDBM ? 1u : 0u;
   uint64_t* dcount = es.count;
   uint64_t* ev = (uint64_t*)(base + o_ev);
   const SpecList spec{(uint64_t*)(base + o_spec), (uint16_t*)(base + o_start)};
-  const bool walk = recs && cap;
+  const bool walk = MDBM || (recs && cap);
+  const uint64_t wcap = recs ? cap : 0;
   const SpadTable sp = make_spad(seed);
-  if (e == hipSuccess) {
-    tsv_a_kernel<<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, es.blk_fn, ev, spec, sp);
-    e = hipGetLastError();
-  }
+  tsv_a_kernel<MDBM><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, es.blk_fn, ev, spec, sp);
+  tr(hipGetLastError());
   if (e == hipSuccess) {
     tsv_scan_kernel<<<(unsigned)ntile, kTThreads, 0, stream>>>(es);
-    e = hipGetLastError();
+    tr(hipGetLastError());
   }
   if (e == hipSuccess && walk) {
-    if (h1)
-      tsv_b_kernel<true><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, es.intile, es.tile_in, ev, spec.raw,
-                                                                   spec.start, dcount, cap, recs, sp, h1, h2);
+    if (h1 && recs)
+      tsv_b_kernel<true, MDBM><<<(unsigned)nblk, kTThreads, 0, stream>>>(
+          f, size, es.intile, es.tile_in, ev, spec.raw, spec.start, dcount, wcap, recs, sp, h1, h2, sc.hflags_d);
     else
-      tsv_b_kernel<false><<<(unsigned)nblk, kTThreads, 0, stream>>>(f, size, es.intile, es.tile_in, ev, spec.raw,
-                                                                    spec.start, dcount, cap, recs, sp, nullptr,
-                                                                    nullptr);
-    e = hipGetLastError();
+      tsv_b_kernel<false, MDBM><<<(unsigned)nblk, kTThreads, 0, stream>>>(
+          f, size, es.intile, es.tile_in, ev, spec.raw, spec.start, dcount, wcap, recs, sp, nullptr, nullptr,
+          sc.hflags_d);
+    tr(hipGetLastError());
   }
   tr(hipStreamSynchronize(stream));
-  const uint64_t n = e == hipSuccess ? __atomic_load_n(sc.hcnt, __ATOMIC_ACQUIRE) : 0;
+  const uint64_t n = e == hipSuccess ? __atomic_load_n(&sc.hflags[0], __ATOMIC_ACQUIRE) : 0;
+  const bool hdr_ok = !MDBM || __atomic_load_n(&sc.hflags[1], __ATOMIC_ACQUIRE) != 0;
+  // mdbm, a last key line at EOF after other records: the previous record's value (rare; a
+  // second synchronisation only then)
+  if (MDBM && e == hipSuccess && hdr_ok && __atomic_load_n(&sc.hflags[2], __ATOMIC_ACQUIRE) && recs && n >= 2 &&
+      n <= cap) {
+    tr(hipMemcpyAsync(&recs[n - 1].val_off, &recs[n - 2].val_off, 16, hipMemcpyDeviceToDevice, stream));
+    tr(hipStreamSynchronize(stream));
+  }
   if (sc.bytes > kScratchKeep) {  // the stream is synchronised: no kernel still reads it
     (void)hipFree(sc.p);
     sc.p = nullptr;
@@ -1025,6 +949,7 @@ static int launch_tsv(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs,
   }
   *herr = e;
   if (e != hipSuccess) return K2H_AMD_EHIP;
+  if (!hdr_ok) return K2H_AMD_EINVAL;  // k2himport: "error: not a mdbm file."
   *count = n;
   return (recs && n > cap) ? K2H_AMD_EINVAL : K2H_AMD_OK;
 }
@@ -1038,95 +963,8 @@ int launch_import_scan(const void* file, uint64_t size, int format, k2h_amd_impo
   *count = 0;
   // an empty file: no records (TSV), or no header (mdbm: "not a mdbm file"); no device work
   if (size == 0) return format == K2H_AMD_IMPORT_TSV ? K2H_AMD_OK : K2H_AMD_EINVAL;
-  const uint64_t nblk = (size + kChunk - 1) / kChunk;
-  if (nblk > 0x7FFFFFFFull) return K2H_AMD_EINVAL;
-  if (format == K2H_AMD_IMPORT_TSV) return launch_tsv(f, size, recs, cap, count, stream, herr, h1, h2, seed);
-  // mdbm
-  uint64_t *bcnt = nullptr, *bbase = nullptr, *nl = nullptr, *lnul = nullptr;
-  void* tmp = nullptr;
-  size_t tmp_bytes = 0;
-  uint32_t *bst = nullptr, *bin = nullptr;
-  uint64_t nnl = 0, nlines = 0, nrec = 0;
-  int rc = K2H_AMD_OK;
-  hipError_t e = hipSuccess;
-#define K2H_TRY(x) \
-  do {             \
-    if (e == hipSuccess) e = (x); \
-  } while (0)
-  K2H_TRY(scratch_alloc((void**)&bcnt, nblk * 8, stream));
-  K2H_TRY(scratch_alloc((void**)&bbase, (nblk + 1) * 8, stream));
-  K2H_TRY(scratch_alloc((void**)&bst, nblk * 4, stream));
-  K2H_TRY(scratch_alloc((void**)&bin, nblk * 4, stream));
-  if (e == hipSuccess) {
-    span_count_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bcnt, bst);
-    e = hipGetLastError();
-  }
-  K2H_TRY(hipMemsetAsync(bbase, 0, 8, stream));
-  size_t t1 = 0, t2 = 0;
-  K2H_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, t1, bcnt, bbase + 1, nblk, stream));
-  K2H_TRY(hipcub::DeviceScan::ExclusiveScan(nullptr, t2, bst, bin, SpanOp(), 0u, nblk, stream));
-  tmp_bytes = t1 > t2 ? t1 : t2;
-  K2H_TRY(scratch_alloc(&tmp, tmp_bytes ? tmp_bytes : 1, stream));
-  K2H_TRY(hipcub::DeviceScan::InclusiveSum(tmp, t1, bcnt, bbase + 1, nblk, stream));
-  K2H_TRY(hipcub::DeviceScan::ExclusiveScan(tmp, t2, bst, bin, SpanOp(), 0u, nblk, stream));
-  // one read-back: newline count, last byte
-  uint64_t sum[2] = {0, '\n'};
-  uint64_t* dsum = nullptr;
-  K2H_TRY(scratch_alloc((void**)&dsum, sizeof sum, stream));
-  if (e == hipSuccess) {
-    scan_summary_kernel<<<1, 1, 0, stream>>>(f, size, bbase, nblk, dsum);
-    e = hipGetLastError();
-  }
-  K2H_TRY(hipMemcpyAsync(sum, dsum, sizeof sum, hipMemcpyDeviceToHost, stream));
-  K2H_TRY(hipStreamSynchronize(stream));
-  if (dsum) (void)hipFreeAsync(dsum, stream);
-  nnl = sum[0];
-  nlines = nnl + ((uint8_t)sum[1] != '\n' ? 1 : 0);  // the bytes after the last newline, if any
-  K2H_TRY(scratch_alloc((void**)&nl, (nnl ? nnl : 1) * 8, stream));
-  K2H_TRY(scratch_alloc((void**)&lnul, (nlines ? nlines : 1) * 8, stream));
-  if (nlines) K2H_TRY(hipMemsetAsync(lnul, 0xFF, nlines * 8, stream));  // kNone
-  if (e == hipSuccess) {
-    span_write_kernel<<<(unsigned)nblk, kThreads, 0, stream>>>(f, size, bbase, bin, nl, lnul);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) {
-    // header: five getline calls; the fifth must extract exactly "HEADER=END"
-    static const char kEnd[] = "HEADER=END";
-    uint64_t hb = 0, he = 0, body = 0;
-    bool ok = nlines >= 5;
-    if (ok) {
-      uint64_t pos[5] = {0, 0, 0, 0, 0};
-      const uint64_t m = nnl < 5 ? nnl : 5;
-      if (m) K2H_TRY(hipMemcpyAsync(pos, nl, m * 8, hipMemcpyDeviceToHost, stream));
-      K2H_TRY(hipStreamSynchronize(stream));
-      hb = pos[3] + 1;
-      he = nnl >= 5 ? pos[4] : size;  // the fifth line may end at EOF
-      body = nnl >= 5 ? pos[4] + 1 : size;
-      char hdr[sizeof kEnd] = {0};
-      ok = he - hb == sizeof kEnd - 1;
-      if (ok) K2H_TRY(hipMemcpyAsync(hdr, f + hb, sizeof kEnd - 1, hipMemcpyDeviceToHost, stream));
-      K2H_TRY(hipStreamSynchronize(stream));
-      ok = ok && memcmp(hdr, kEnd, sizeof kEnd - 1) == 0;
-    }
-    if (e == hipSuccess && !ok) rc = K2H_AMD_EINVAL;  // k2himport: "error: not a mdbm file."
-    if (e == hipSuccess && ok) {
-      nrec = nlines > 5 ? (nlines - 5 + 1) / 2 : 0;
-      if (recs && nrec && nrec <= cap) {
-        mdbm_records_kernel<<<blocks_for(nrec), kThreads, 0, stream>>>(nl, nnl, size, lnul, nlines, nrec, body,
-                                                                          recs, f, make_spad(seed), h1, h2);
-        e = hipGetLastError();
-      }
-    }
-  }
-  K2H_TRY(hipStreamSynchronize(stream));
-#undef K2H_TRY
-  for (void* p : {(void*)bcnt, (void*)bbase, (void*)bst, (void*)bin, (void*)nl, (void*)lnul, tmp})
-    if (p) (void)hipFreeAsync(p, stream);
-  *herr = e;
-  if (e != hipSuccess) return K2H_AMD_EHIP;
-  if (rc != K2H_AMD_OK) return rc;
-  *count = nrec;
-  return (recs && nrec > cap) ? K2H_AMD_EINVAL : K2H_AMD_OK;
+  if (format == K2H_AMD_IMPORT_TSV) return launch_scan<false>(f, size, recs, cap, count, stream, herr, h1, h2, seed);
+  return launch_scan<true>(f, size, recs, cap, count, stream, herr, h1, h2, seed);
 }
 
 hipError_t launch_import_prehash(const void* file, uint64_t size, const k2h_amd_import_rec* recs, uint64_t n,
