@@ -186,22 +186,39 @@ __device__ inline TState gapply(const GFn& g, const TState& s) {
   return t;
 }
 
-// Stage block `blk` into lds[16 .. 16 + 16 KiB) with coalesced 16-byte loads (bytes past
-// the file read as 0x01, no event; the 16 bytes below are chunk 0's pad for the hashes).
+// Stage block `blk` into lds[PRE + 16 .. PRE + 16 + 16 KiB) with coalesced 16-byte loads
+// (bytes past the file read as 0x01, no event; the 16 bytes below are chunk 0's pad for
+// the hashes), and the PRE bytes before the block into lds[16 .. 16 + PRE) (block 0: 0x01).
+template <uint32_t PRE>
 __device__ inline void tsv_stage(const uint8_t* __restrict__ f, uint64_t size, uint64_t blk, uint8_t* lds) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const uint64_t base = blk * kTChunk;
   const bool aligned = (((uintptr_t)(f + base)) & 15) == 0;
   constexpr int Q = (int)(kTChunk / 16 / kTThreads);
+  const bool pre = PRE && threadIdx.x < PRE / 16;
+  u32x4 pv = u32x4{0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};
   if (aligned && base + kTChunk <= size) {  // block-uniform: every load in flight at once
     u32x4 v[Q];                              // (a per-piece branch waited for each in turn)
+    if (pre && base) pv = *reinterpret_cast<const u32x4*>(f + base - PRE + 16 * threadIdx.x);
 #pragma unroll
     for (int q = 0; q < Q; ++q)
       v[q] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(f + base + 16ull * (threadIdx.x + kTThreads * q)));
+    if (pre) *reinterpret_cast<u32x4*>(lds + 16 + 16 * threadIdx.x) = pv;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) *reinterpret_cast<u32x4*>(lds + 16 + 16 * (threadIdx.x + kTThreads * q)) = v[q];
+    for (int q = 0; q < Q; ++q) *reinterpret_cast<u32x4*>(lds + PRE + 16 + 16 * (threadIdx.x + kTThreads * q)) = v[q];
     __syncthreads();
     return;
+  }
+  if (pre) {
+    if (base) {
+      const uint8_t* p = f + base - PRE + 16 * threadIdx.x;  // (base >= 16 KiB > PRE)
+      uint32_t x[4];
+      for (int k = 0; k < 4; ++k)
+        x[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
+               ((uint32_t)p[4 * k + 3] << 24);
+      pv = u32x4{x[0], x[1], x[2], x[3]};
+    }
+    *reinterpret_cast<u32x4*>(lds + 16 + 16 * threadIdx.x) = pv;
   }
 #pragma unroll
   for (int q = 0; q < Q; ++q) {
@@ -221,7 +238,7 @@ __device__ inline void tsv_stage(const uint8_t* __restrict__ f, uint64_t size, u
       }
       v = u32x4{x[0], x[1], x[2], x[3]};
     }
-    *reinterpret_cast<u32x4*>(lds + 16 + 16 * piece) = v;
+    *reinterpret_cast<u32x4*>(lds + PRE + 16 + 16 * piece) = v;
   }
   __syncthreads();
 }
@@ -465,30 +482,16 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + PRE + kTChunk];
   __shared__ uint64_t s_key[kListCap];  // emitted keys: start (16-bit, signed) | len << 16
   __shared__ uint32_t s_nk;
+  __shared__ uint32_t s_cls[8];        // keys per chunk-count class, then class offsets
+  __shared__ uint8_t s_ord[kListCap];  // list indices in class order
   typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
   __shared__ typename NlScan::TempStorage tmp;
   __shared__ LFn s_wave[kTThreads / 64];
   if (threadIdx.x == 0) s_nk = 0;
+  if (threadIdx.x < 8) s_cls[threadIdx.x] = 0;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
-  if (!MDBM && threadIdx.x < PRE / 16) {  // the kPre bytes before the block, for its head key
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 v = u32x4{0x01010101u, 0x01010101u, 0x01010101u, 0x01010101u};  // block 0: no event
-    if (base) {
-      const uint8_t* p = f + base - PRE + 16 * threadIdx.x;  // (base >= 16 KiB > PRE)
-      if ((((uintptr_t)p) & 15) == 0) {
-        v = *reinterpret_cast<const u32x4*>(p);
-      } else {
-        uint32_t x[4];
-        for (int k = 0; k < 4; ++k)
-          x[k] = (uint32_t)p[4 * k] | ((uint32_t)p[4 * k + 1] << 8) | ((uint32_t)p[4 * k + 2] << 16) |
-                 ((uint32_t)p[4 * k + 3] << 24);
-        v = u32x4{x[0], x[1], x[2], x[3]};
-      }
-    }
-    *reinterpret_cast<u32x4*>(lds + 16 + 16 * threadIdx.x) = v;
-  }
-  uint8_t* blk = lds + PRE;  // block byte i at blk[16 + i]; the prefix below it
-  tsv_stage(f, size, blockIdx.x, blk);  // (its barrier publishes s_nk = 0 and the prefix)
+  uint8_t* blk = lds + PRE;  // block byte i at blk[16 + i]; the kPre bytes before the block below it
+  tsv_stage<PRE>(f, size, blockIdx.x, lds);  // (its barrier publishes s_nk = 0)
   const uint32_t rel = kTBytes * threadIdx.x;
   const uint8_t* span = blk + 16 + rel;
   const bool live = base + rel < size;
@@ -560,8 +563,38 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   }
   ev[base / kTBytes + threadIdx.x] = pk;
   __syncthreads();
+  // The list's keys in order of chunk count (counting sort over 8 classes), so that each
+  // wave's hash loop runs as long as ITS longest key: on BASELINE-like files (keys 8-64 B,
+  // 1-4 chunks) wave 0 takes the short keys and runs 2 chunks instead of 4 (round 4).
   const uint32_t nk = min(s_nk, kListCap);
-  for (uint32_t i = threadIdx.x; i < nk; i += kTThreads) {
+  static_assert(kListCap <= 2 * kTThreads, "two list keys per thread");
+  uint32_t cls[2];
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h) {
+    const uint32_t i = threadIdx.x + h * kTThreads;
+    cls[h] = i < nk ? min(((uint32_t)(s_key[i] >> 16) & 0xFFFFu) + 15u, 128u) / 16u : 0u;  // 0..8
+    cls[h] = cls[h] ? cls[h] - 1u : 0u;
+    if (i < nk) atomicAdd(&s_cls[cls[h]], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (uint32_t c = 0; c < 8; ++c) {
+      const uint32_t v = s_cls[c];
+      s_cls[c] = acc;
+      acc += v;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h) {
+    const uint32_t i = threadIdx.x + h * kTThreads;
+    if (i < nk) s_ord[atomicAdd(&s_cls[cls[h]], 1u)] = (uint8_t)i;
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < nk; q += kTThreads) {
+    const uint32_t i = s_ord[q];
     const uint64_t k = s_key[i];
     const int32_t st = (int16_t)(k & 0xFFFFu);
     const uint32_t len = (uint32_t)(k >> 16) & 0xFFFFu;
