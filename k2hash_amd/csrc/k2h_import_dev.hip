@@ -113,6 +113,9 @@ unsigned blocks_for(uint64_t n) { return (unsigned)((n + kThreads - 1) / kThread
 constexpr uint32_t kTThreads = 128;
 constexpr uint32_t kTBytes = 128;                               // bytes per thread
 constexpr uint32_t kTChunk = kTThreads * kTBytes;               // 16 KiB per block
+// pass B (and the entry-state scan) works in units of one wave's spans: 8 KiB
+constexpr uint32_t kUnit = 64 * kTBytes;
+constexpr uint32_t kUnitsPerBlock = kTChunk / kUnit;
 
 // Block-local function of a span; positions are block-relative + 1 (0: none).  Every
 // field is a pair of 16-bit halves, low = entering in K, high = entering in V:
@@ -389,10 +392,12 @@ struct NlOp {
   __device__ uint32_t operator()(uint32_t x, uint32_t y) const { return nl_compose(NlSum{x}, NlSum{y}).v; }
 };
 
-// The block's function: pass A needs only the reduction of its span functions (pass B
-// rebuilds the per-span prefixes), so an order-preserving shuffle-down tree per wave and
-// the two wave results composed in order -- about half a block scan's instructions.
-__device__ inline LFn block_fn_reduce(LFn r, LFn* s_wave) {
+// A wave's function (lane 0's result): pass A needs only the reduction of its span
+// functions (pass B rebuilds the per-span prefixes), so an order-preserving shuffle-down
+// tree -- about half a scan's instructions.  Each wave of pass A writes its own 8 KiB
+// unit's function (round 4: pass B runs one wave per unit, so its scan is a wave scan with
+// no LDS or barrier; round 3 composed the two wave results into a per-block function).
+__device__ inline LFn wave_fn_reduce(LFn r) {
   const uint32_t lane = threadIdx.x & 63u;
 #pragma unroll
   for (uint32_t off = 1; off < 64; off <<= 1) {
@@ -401,12 +406,7 @@ __device__ inline LFn block_fn_reduce(LFn r, LFn* s_wave) {
     const LFn c = LCompose()(r, y);
     if (lane + off < 64) r = c;
   }
-  if (lane == 0) s_wave[threadIdx.x >> 6] = r;
-  __syncthreads();
-  LFn t = s_wave[0];
-#pragma unroll
-  for (uint32_t w = 1; w < kTThreads / 64; ++w) t = LCompose()(t, s_wave[w]);
-  return t;
+  return r;
 }
 
 // Entry states of the blocks (tsv_scan_kernel, one launch instead of a device scan and a
@@ -418,7 +418,7 @@ __device__ inline LFn block_fn_reduce(LFn r, LFn* s_wave) {
 constexpr uint32_t kTilePer = 4;
 constexpr uint32_t kTile = kTilePer * kTThreads;  // blocks per tile
 struct EntryScan {
-  GFn* blk_fn;         // [nblk] each block's function
+  GFn* blk_fn;         // [nblk] each unit's function (8 KiB units; "blocks" of the scan)
   GFn* intile;         // [nblk] exclusive prefix of its function within its tile
   GFn* tile_fn;        // [ntile]
   TState* tile_in;     // [ntile] state entering the tile
@@ -486,7 +486,6 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __shared__ uint8_t s_ord[kListCap];  // list indices in class order
   typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
   __shared__ typename NlScan::TempStorage tmp;
-  __shared__ LFn s_wave[kTThreads / 64];
   if (threadIdx.x == 0) s_nk = 0;
   if (threadIdx.x < 8) s_cls[threadIdx.x] = 0;
   const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
@@ -508,8 +507,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     });
   const bool over = ne > kEvCap;
   pk = over ? kEvOverflow : pk | ((uint64_t)ne << 45) | kNoSlots;
-  const LFn bf = block_fn_reduce(acc, s_wave);
-  if (threadIdx.x == 0) blk_fn[blockIdx.x] = gfn_of(bf, base);
+  const LFn wf = wave_fn_reduce(acc);
+  if ((threadIdx.x & 63u) == 0) blk_fn[(uint64_t)blockIdx.x * kUnitsPerBlock + (threadIdx.x >> 6)] = gfn_of(wf, base);
   if constexpr (MDBM) {
     ev[base / kTBytes + threadIdx.x] = pk;
     return;
@@ -653,7 +652,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_scan_kernel(EntryScan es) {
 // (getline leaves the string as it was when it fails at EOF) -- the first record's
 // directly, any later one by the host after the call (hflags[2], a 16-byte copy).
 template <bool HASH, bool MDBM>
-__global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restrict__ f, uint64_t size,
+__global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                           const GFn* __restrict__ intile,
                                                           const TState* __restrict__ tile_in,
                                                           const uint64_t* __restrict__ ev,
@@ -663,10 +662,12 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
                                                           k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
                                                           uint64_t* __restrict__ h1, uint64_t* __restrict__ h2,
                                                           uint64_t* __restrict__ hflags) {
-  typedef hipcub::BlockScan<LFn, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> Scan;
+  // one wave per 8 KiB unit: the span functions' prefix is a wave scan (no LDS, no barrier)
+  typedef hipcub::WarpScan<LFn, 64> Scan;
   __shared__ typename Scan::TempStorage tmp;
   constexpr uint64_t HDR = MDBM ? kHdrRecs : 0;
-  const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
+  const uint64_t base = (uint64_t)blockIdx.x * kUnit;
+  const uint64_t blk = blockIdx.x / kUnitsPerBlock, blk_base = blk * kTChunk;  // pass A's block (spec list)
   const uint32_t rel = kTBytes * threadIdx.x;
   const bool live = base + rel < size;
   const uint64_t ti = base / kTBytes + threadIdx.x;
@@ -683,8 +684,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
     sl_start[j] = 0xFFFFFFFFu;
     const uint32_t li = (uint32_t)(pk >> (48 + 8 * j)) & 0xFFu;
     if (HASH && !MDBM && li != 0xFFu) {
-      sl_raw[j] = spec_raw[(uint64_t)blockIdx.x * kListCap + li];
-      sl_start[j] = spec_start[(uint64_t)blockIdx.x * kListCap + li];
+      sl_raw[j] = spec_raw[blk * kListCap + li];
+      sl_start[j] = spec_start[blk * kListCap + li];
     }
   }
   // a span with more than kEvCap events (rare): its candidate masks from the file, each
@@ -761,7 +762,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_b_kernel(const uint8_t* __restr
       uint64_t a, c;
       // the key's start relative to the block as pass A stored it (16 bits; a key that
       // starts in the bytes before the block, pass A's head key, is negative)
-      const uint32_t want = s.fs + kTChunk >= base ? (uint32_t)((s.fs - base) & 0xFFFFu) : 0xFFFFFFFEu;
+      const uint32_t want = s.fs + kTChunk >= blk_base ? (uint32_t)((s.fs - blk_base) & 0xFFFFu) : 0xFFFFFFFEu;
       bool hit = false;
       uint64_t raw = 0;
 #pragma unroll
@@ -891,8 +892,10 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
     *herr = e;
     return K2H_AMD_EHIP;
   }
-  const uint64_t ntile = (nblk + kTile - 1) / kTile;
-  const size_t o_fn = 0, o_in = o_fn + align256(nblk * sizeof(GFn)), o_tf = o_in + align256(nblk * sizeof(GFn));
+  const uint64_t nunit = (size + kUnit - 1) / kUnit;  // pass B's waves and the scan's items
+  const uint64_t ntile = (nunit + kTile - 1) / kTile;
+  const size_t nfn = nblk * kUnitsPerBlock;  // pass A writes every wave's function, past-EOF ones too
+  const size_t o_fn = 0, o_in = o_fn + align256(nfn * sizeof(GFn)), o_tf = o_in + align256(nfn * sizeof(GFn));
   const size_t o_ti = o_tf + align256(ntile * sizeof(GFn)), o_ev = o_ti + align256(ntile * sizeof(TState));
   const size_t nspec = MDBM ? 0 : nblk * kListCap;
   const size_t o_spec = o_ev + align256(nblk * kTThreads * 8), o_start = o_spec + align256(nspec * 8);
@@ -939,7 +942,7 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
   es.done = (uint32_t*)cb;
   es.count = (uint64_t*)(cb + 8);
   es.host_count = sc.hflags_d;
-  es.nblk = nblk;
+  es.nblk = nunit;
   es.ntile = ntile;
   es.size = size;
   es.mdbm = MDBM ? 1u : 0u;
@@ -957,10 +960,10 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
   }
   if (e == hipSuccess && walk) {
     if (h1 && recs)
-      tsv_b_kernel<true, MDBM><<<(unsigned)nblk, kTThreads, 0, stream>>>(
+      tsv_b_kernel<true, MDBM><<<(unsigned)nunit, 64, 0, stream>>>(
           f, size, es.intile, es.tile_in, ev, spec.raw, spec.start, dcount, wcap, recs, sp, h1, h2, sc.hflags_d);
     else
-      tsv_b_kernel<false, MDBM><<<(unsigned)nblk, kTThreads, 0, stream>>>(
+      tsv_b_kernel<false, MDBM><<<(unsigned)nunit, 64, 0, stream>>>(
           f, size, es.intile, es.tile_in, ev, spec.raw, spec.start, dcount, wcap, recs, sp, nullptr, nullptr,
           sc.hflags_d);
     tr(hipGetLastError());
