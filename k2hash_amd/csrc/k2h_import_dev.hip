@@ -480,7 +480,10 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
                                                           SpecList spec, SpadTable sp) {
   constexpr uint32_t PRE = MDBM ? 0u : kPre;
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + PRE + kTChunk];
-  __shared__ uint64_t s_key[kListCap];  // emitted keys: start (16-bit, signed) | len << 16
+  // emitted keys: start (16-bit, signed) | len << 16 (32 bits: the block's LDS must stay
+  // within 17.5 KiB for 9 blocks per CU -- 18 KiB, one 512-byte granule more, gave 8 and
+  // cost pass A 11 %, round 4)
+  __shared__ uint32_t s_key[kListCap];
   __shared__ uint32_t s_nk;
   __shared__ uint32_t s_cls[8];        // keys per chunk-count class, then class offsets
   __shared__ uint8_t s_ord[kListCap];  // list indices in class order
@@ -551,7 +554,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
         }
         const uint32_t slot = ok ? atomicAdd(&s_nk, 1u) : kListCap;
         if (slot < kListCap) {
-          s_key[slot] = ((uint32_t)start & 0xFFFFu) | ((uint64_t)((int32_t)pos - start) << 16);
+          s_key[slot] = ((uint32_t)start & 0xFFFFu) | ((uint32_t)((int32_t)pos - start) << 16);
           pk = (pk & ~(0xFFull << (48 + 8 * j))) | ((uint64_t)slot << (48 + 8 * j));
         }
       }
@@ -571,7 +574,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
 #pragma unroll
   for (uint32_t h = 0; h < 2; ++h) {
     const uint32_t i = threadIdx.x + h * kTThreads;
-    cls[h] = i < nk ? min(((uint32_t)(s_key[i] >> 16) & 0xFFFFu) + 15u, 128u) / 16u : 0u;  // 0..8
+    cls[h] = i < nk ? min((s_key[i] >> 16) + 15u, 128u) / 16u : 0u;  // 0..8
     cls[h] = cls[h] ? cls[h] - 1u : 0u;
     if (i < nk) atomicAdd(&s_cls[cls[h]], 1u);
   }
@@ -594,9 +597,9 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < nk; q += kTThreads) {
     const uint32_t i = s_ord[q];
-    const uint64_t k = s_key[i];
+    const uint32_t k = s_key[i];
     const int32_t st = (int16_t)(k & 0xFFFFu);
-    const uint32_t len = (uint32_t)(k >> 16) & 0xFFFFu;
+    const uint32_t len = k >> 16;
     spec.raw[(uint64_t)blockIdx.x * kListCap + i] = key_raw_lds(blk + 16 + st, len, sp);
     spec.start[(uint64_t)blockIdx.x * kListCap + i] = (uint16_t)(k & 0xFFFFu);
   }
