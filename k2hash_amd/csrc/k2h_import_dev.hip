@@ -397,16 +397,11 @@ struct NlOp {
 // tree -- about half a scan's instructions.  Each wave of pass A writes its own 8 KiB
 // unit's function (round 4: pass B runs one wave per unit, so its scan is a wave scan with
 // no LDS or barrier; round 3 composed the two wave results into a per-block function).
-__device__ inline LFn wave_fn_reduce(LFn r) {
-  const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-  for (uint32_t off = 1; off < 64; off <<= 1) {
-    const LFn y{(uint32_t)__shfl_down((int)r.sel, off, 64), (uint32_t)__shfl_down((int)r.cnt, off, 64),
-                (uint32_t)__shfl_down((int)r.last, off, 64), (uint32_t)__shfl_down((int)r.c, off, 64)};
-    const LFn c = LCompose()(r, y);
-    if (lane + off < 64) r = c;
-  }
-  return r;
+// (hipcub's warp reduction: DPP row shifts and lane permutes; the round-3 __shfl_down tree
+// compiled to 24 ds_bpermute per lane)
+template <class Tmp>
+__device__ inline LFn wave_fn_reduce(Tmp& tmp, LFn r) {
+  return hipcub::WarpReduce<LFn, 64>(tmp).Reduce(r, LCompose());
 }
 
 // Entry states of the blocks (tsv_scan_kernel, one launch instead of a device scan and a
@@ -486,6 +481,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __shared__ uint32_t s_key[kListCap];
   __shared__ uint32_t s_nk;
   __shared__ uint32_t s_cls[8];        // keys per chunk-count class, then class offsets
+  __shared__ typename hipcub::WarpReduce<LFn, 64>::TempStorage s_wred[kTThreads / 64];
   __shared__ uint8_t s_ord[kListCap];  // list indices in class order
   typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
   __shared__ typename NlScan::TempStorage tmp;
@@ -510,7 +506,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     });
   const bool over = ne > kEvCap;
   pk = over ? kEvOverflow : pk | ((uint64_t)ne << 45) | kNoSlots;
-  const LFn wf = wave_fn_reduce(acc);
+  const LFn wf = wave_fn_reduce(s_wred[threadIdx.x >> 6], acc);
   if ((threadIdx.x & 63u) == 0) blk_fn[(uint64_t)blockIdx.x * kUnitsPerBlock + (threadIdx.x >> 6)] = gfn_of(wf, base);
   if constexpr (MDBM) {
     ev[base / kTBytes + threadIdx.x] = pk;
