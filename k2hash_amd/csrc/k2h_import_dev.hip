@@ -413,8 +413,8 @@ __device__ inline LFn wave_fn_reduce(Tmp& tmp, LFn r) {
 constexpr uint32_t kTilePer = 4;
 constexpr uint32_t kTile = kTilePer * kTThreads;  // blocks per tile
 struct EntryScan {
-  GFn* blk_fn;         // [nblk] each unit's function (8 KiB units; "blocks" of the scan)
-  GFn* intile;         // [nblk] exclusive prefix of its function within its tile
+  GFn* blk_fn;         // [2 nblk] each pass-B unit's (pass A wave's) function
+  GFn* intile;         // [2 nblk] exclusive prefix of each unit's function within its tile
   GFn* tile_fn;        // [ntile]
   TState* tile_in;     // [ntile] state entering the tile
   uint32_t* done;      // tiles finished, zero between calls
@@ -430,23 +430,23 @@ struct EntryScan {
 // fifth header line is record 2's value line (checked in pass B).
 constexpr uint64_t kHdrRecs = 3;
 
-// Exclusive scan of in[0, n) by one block, thread t owning the run [t k, (t + 1) k):
-// out(i, prefix of in[0, i)); returns the whole reduction.  Runs of up to 4 are loaded
+// Exclusive scan of in(0) .. in(n - 1) by one block, thread t owning the run [t k, (t + 1) k):
+// out(i, prefix of in(0 .. i - 1)); returns the whole reduction.  Runs of up to 4 are loaded
 // at once and kept in registers (the tile scan's 4 and the tile-level scan of files up to
 // 4 GiB); longer runs re-read their elements.
-template <class Tmp, class Out>
-__device__ inline GFn block_scan_runs(Tmp& tmp, const GFn* in, uint64_t n, uint64_t k, Out&& out) {
+template <class Tmp, class In, class Out>
+__device__ inline GFn block_scan_runs(Tmp& tmp, In&& in, uint64_t n, uint64_t k, Out&& out) {
   typedef hipcub::BlockScan<GFn, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> GScan;
   const uint64_t i0 = (uint64_t)threadIdx.x * k, i1 = min(i0 + k, n);
   GFn x[4];
   GFn loc = gfn_id();
   if (k <= 4) {
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) x[q] = i0 + q < i1 ? in[i0 + q] : gfn_id();
+    for (uint32_t q = 0; q < 4; ++q) x[q] = i0 + q < i1 ? in(i0 + q) : gfn_id();
 #pragma unroll
     for (uint32_t q = 0; q < 4; ++q) loc = GCompose()(loc, x[q]);
   } else {
-    for (uint64_t i = i0; i < i1; ++i) loc = GCompose()(loc, in[i]);
+    for (uint64_t i = i0; i < i1; ++i) loc = GCompose()(loc, in(i));
   }
   GFn pre, agg;
   GScan(tmp).ExclusiveScan(loc, pre, gfn_id(), GCompose(), agg);
@@ -460,7 +460,7 @@ __device__ inline GFn block_scan_runs(Tmp& tmp, const GFn* in, uint64_t n, uint6
   } else {
     for (uint64_t i = i0; i < i1; ++i) {
       out(i, pre);
-      pre = GCompose()(pre, in[i]);
+      pre = GCompose()(pre, in(i));
     }
   }
   return agg;
@@ -611,8 +611,16 @@ __global__ __launch_bounds__(kTThreads) void tsv_scan_kernel(EntryScan es) {
   __shared__ typename GScan::TempStorage gtmp;
   __shared__ uint32_t s_last;
   const uint64_t tile = blockIdx.x, b0 = tile * kTile;
-  const GFn tf = block_scan_runs(gtmp, es.blk_fn + b0, min<uint64_t>(kTile, es.nblk - b0), kTilePer,
-                                 [&](uint64_t i, const GFn& p) { es.intile[b0 + i] = p; });
+  // items are pass A's blocks, each the composition of its two waves' functions; each
+  // block's prefix is written for both of its pass-B units (the second one past wave 0)
+  const GFn* wfn = es.blk_fn + kUnitsPerBlock * b0;
+  const GFn tf = block_scan_runs(
+      gtmp, [&](uint64_t i) { return GCompose()(wfn[2 * i], wfn[2 * i + 1]); },
+      min<uint64_t>(kTile, es.nblk - b0), kTilePer, [&](uint64_t i, const GFn& p) {
+        es.intile[kUnitsPerBlock * (b0 + i)] = p;
+        es.intile[kUnitsPerBlock * (b0 + i) + 1] = GCompose()(p, wfn[2 * i]);
+      });
+  static_assert(kUnitsPerBlock == 2, "two pass-B units per pass-A block");
   if (threadIdx.x == 0) {
     es.tile_fn[tile] = tf;
     __threadfence();
@@ -623,7 +631,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_scan_kernel(EntryScan es) {
   __threadfence();  // acquire: every tile's function
   const uint64_t k = (es.ntile + kTThreads - 1) / kTThreads;
   const TState s0{es.mdbm, 0, 0, 0};
-  const GFn all = block_scan_runs(gtmp, es.tile_fn, es.ntile, k,
+  const GFn all = block_scan_runs(gtmp, [&](uint64_t i) { return es.tile_fn[i]; }, es.ntile, k,
                                   [&](uint64_t i, const GFn& p) { es.tile_in[i] = gapply(p, s0); });
   if (threadIdx.x == 0) {
     const TState e = gapply(all, s0);
@@ -672,7 +680,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   const uint64_t ti = base / kTBytes + threadIdx.x;
   const uint64_t pk = ev[ti];
   const GFn ein = intile[blockIdx.x];
-  const TState tin = tile_in[blockIdx.x / kTile];
+  const TState tin = tile_in[blk / kTile];
   const bool over = ev_count(pk) == 7u;
   // the slots pass A wrote for this span, loaded now so their latency hides under the scan
   uint64_t sl_raw[kSlots];
@@ -892,7 +900,7 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
     return K2H_AMD_EHIP;
   }
   const uint64_t nunit = (size + kUnit - 1) / kUnit;  // pass B's waves and the scan's items
-  const uint64_t ntile = (nunit + kTile - 1) / kTile;
+  const uint64_t ntile = (nblk + kTile - 1) / kTile;  // tiles of pass-A blocks
   const size_t nfn = nblk * kUnitsPerBlock;  // pass A writes every wave's function, past-EOF ones too
   const size_t o_fn = 0, o_in = o_fn + align256(nfn * sizeof(GFn)), o_tf = o_in + align256(nfn * sizeof(GFn));
   const size_t o_ti = o_tf + align256(ntile * sizeof(GFn)), o_ev = o_ti + align256(ntile * sizeof(TState));
@@ -941,7 +949,7 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
   es.done = (uint32_t*)cb;
   es.count = (uint64_t*)(cb + 8);
   es.host_count = sc.hflags_d;
-  es.nblk = nunit;
+  es.nblk = nblk;
   es.ntile = ntile;
   es.size = size;
   es.mdbm = MDBM ? 1u : 0u;
