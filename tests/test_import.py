@@ -332,3 +332,32 @@ def test_fused_scan_prehash_concurrent_threads(cuda, oracle):
 
     with concurrent.futures.ThreadPoolExecutor(4) as ex:
         assert all(ex.map(work, range(4)))
+
+
+@pytest.mark.gpu
+def test_fused_scan_prehash_many_unspeculated_keys(cuda, oracle):
+    """Keys pass A cannot speculate (each holds a newline, so the key does not start after
+    the last newline before its TAB) are hashed by pass B from the file: 300,000 such
+    records plus ordinary ones, records and hashes equal to the host scan and the reference
+    (round 4 tried moving these misses into per-wave lists for a separate kernel; it lost,
+    profiles/r04k_import_misslist_ab.txt, and this test covered it)."""
+    import torch
+    rng = np.random.default_rng(29)
+    parts = []
+    for i in range(300000):
+        parts.append(b"k%d\nx\t%d\n" % (i, int(rng.integers(0, 1000))))
+        if i % 1000 == 0:
+            parts.append(b"plain%d\tvalue\n" % i)
+    data = b"".join(parts)
+    host = archive.import_scan(data, "tsv")
+    f = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda)
+    recs, h1, h2 = archive.import_scan_prehash_device(f, "tsv")
+    torch.cuda.synchronize()
+    a = recs.cpu().numpy().view(np.uint64)
+    assert a.shape[0] == host.size > 300000
+    for i, name in enumerate(archive.IMPORT_DTYPE.names):
+        assert np.array_equal(a[:, i], host[name])
+    keys = [data[int(o):int(o) + int(n)] + b"\0" for o, n in zip(host["key_off"], host["key_len"])]
+    assert np.array_equal(h1.cpu().numpy().view(np.uint64), np.array([oracle.k2h_hash(k) for k in keys], np.uint64))
+    assert np.array_equal(h2.cpu().numpy().view(np.uint64),
+                          np.array([oracle.k2h_second_hash(k) for k in keys], np.uint64))
