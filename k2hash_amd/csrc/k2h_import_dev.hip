@@ -246,25 +246,62 @@ __device__ inline void tsv_stage(const uint8_t* __restrict__ f, uint64_t size, u
   __syncthreads();
 }
 
-// Candidate event bytes (value < 0x0B: NUL, TAB, newline and the rare 0x01-0x08) of the
-// thread's 128 bytes as two 64-bit masks, one bit per byte.
+// Candidate event bytes (value < 0x0B: NUL, TAB, newline and the rare 0x01-0x08) of a
+// span's 32 words as two 64-bit masks, one bit per byte in byte order.  Each word's
+// candidates are bit 7 of its bytes (three ops); a v_dot4_u32_u8 gathers two words' eight
+// bits into one byte (multipliers 1, 2, 4, 8 and 16, 32, 64, 128), shifted left by 7.
+// (Round 3: a v_mul_lo_u32 nibble gather per word, a quarter-rate multiply, ~7.7 VALU per
+// word; now ~4.5.)
+__device__ inline uint32_t cand_bits(uint32_t w) {
+  return ~(((w & 0x7F7F7F7Fu) + 0x75757575u) | w) & 0x80808080u;  // bit 7 of each byte < 0x0B
+}
+__device__ inline void cand_masks(const uint32_t (&w)[32], uint64_t& m0, uint64_t& m1) {
+  uint32_t mk[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    uint32_t r[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int p = 4 * k + i;  // bytes [8p, 8p + 8)
+      r[i] = __builtin_amdgcn_udot4(cand_bits(w[2 * p + 1]), 0x80402010u,
+                                    __builtin_amdgcn_udot4(cand_bits(w[2 * p]), 0x08040201u, 0u, false), false);
+    }
+    mk[k] = (r[0] >> 7) | (r[1] << 1) | (r[2] << 9) | (r[3] << 17);
+  }
+  m0 = mk[0] | ((uint64_t)mk[1] << 32);
+  m1 = mk[2] | ((uint64_t)mk[3] << 32);
+}
+// ... of the thread's 128 bytes staged in LDS.  The spans of a wave's lanes lie 128 B apart,
+// so the lanes of a ds_read_b128 group (16 lanes, banks (a / 4) mod 64) reading the same
+// 16-byte piece of their spans hit two bank sets: 8-way conflicts, 32 LDS cycles per read
+// instead of 4 (SQ_LDS_BANK_CONFLICT 46 M cycles per call, round 4).  Lane l reads its
+// pieces starting at piece (l / 2) mod 8 instead -- within every group of 16 lanes (their
+// indices are distinct mod 16) each lane then has its own (span parity, piece) pair and its
+// own four banks -- and the mask is rotated back: read slot q holds piece (q + s) mod 8,
+// so the masks in slot order are the span's rotated right by 16 s bits.
 __device__ inline void tsv_events(const uint8_t* span, uint64_t& m0, uint64_t& m1) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  uint32_t nib[4] = {0, 0, 0, 0};
+  const uint32_t s = (threadIdx.x >> 1) & 7u;
+  uint32_t w[32];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(span + 16 * q);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint32_t small = ~(((w[j] & 0x7F7F7F7Fu) + 0x75757575u) | w[j]) & 0x80808080u;  // bytes < 0x0B
-      const uint32_t n4 = (small * 0x00204081u) >> 28;  // bits 7, 15, 23, 31 -> 0..3
-      const int word = 4 * q + j;                       // 0..31
-      nib[word >> 3] |= n4 << (4 * (word & 7));
-    }
+    const u32x4 v = *reinterpret_cast<const u32x4*>(span + 16 * ((q + s) & 7u));
+    w[4 * q] = v.x, w[4 * q + 1] = v.y, w[4 * q + 2] = v.z, w[4 * q + 3] = v.w;
   }
-  m0 = nib[0] | ((uint64_t)nib[1] << 32);
-  m1 = nib[2] | ((uint64_t)nib[3] << 32);
+  uint64_t r0, r1;
+  cand_masks(w, r0, r1);
+  // rotate the 128 bits left by 16 s: whole dwords by s / 2, then 16 bits if s is odd
+  uint32_t d[4] = {(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
+  uint32_t e[4];
+  const bool t2 = s & 4u, t1 = s & 2u, odd = s & 1u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = t2 ? d[(i + 2) & 3] : d[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) d[i] = t1 ? e[(i + 3) & 3] : e[i];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) e[i] = odd ? __builtin_amdgcn_alignbit(d[i], d[(i + 3) & 3], 16) : d[i];
+  m0 = e[0] | ((uint64_t)e[1] << 32);
+  m1 = e[2] | ((uint64_t)e[3] << 32);
 }
 
 // Consume the lowest event of the 128-bit mask pair: its offset, or 128 when none is left.
@@ -281,9 +318,8 @@ __device__ inline uint32_t next_event(uint64_t& m0, uint64_t& m1) {
 // Events of a thread's span: NL / TAB / NUL bytes (types 1 / 2 / 3) in byte order.  Pass A
 // packs up to kEvCap of them into one word per thread for pass B: entry j = offset (7 bits)
 // | type << 7 at bits [9j, 9j + 9), the count at bits [45, 48) (7 = more than kEvCap: pass B
-// reads the span back from the file), the list index of the span's speculative keys at bits
-// [48, 56) and [56, 64) (0xFF: none; see kSlots)
-// (pass B re-reads that span from the file).
+// reads the span back from the file), and the lengths of the keys pass A hashed for the
+// span's first two cut events at bits [48, 56) and [56, 64) (0xFF: none; see kSlots).
 constexpr uint32_t kEvCap = 5;
 constexpr uint64_t kNoSlots = 0xFFFFull << 48;
 constexpr uint64_t kEvOverflow = (7ull << 45) | kNoSlots;
@@ -293,6 +329,11 @@ __device__ inline uint32_t ev_count(uint64_t pk) { return (uint32_t)(pk >> 45) &
 template <bool MDBM>
 __device__ inline uint32_t ev_type(uint32_t c) {
   return c < 11u ? ((MDBM ? 0x100003u : 0x180003u) >> (2 * c)) & 3u : 0u;
+}
+// ... of a candidate byte (c < 11, as the masks guarantee)
+template <bool MDBM>
+__device__ inline uint32_t cand_type(uint32_t c) {
+  return ((MDBM ? 0x100003u : 0x180003u) >> (2 * c)) & 3u;
 }
 
 // The function of one event at position p1 (block-relative + 1), composed onto a span's
@@ -316,6 +357,21 @@ __device__ inline LFn ev_fn(uint32_t t, uint32_t p1) {
              nl ? 0x10000u : 0u, nl ? p1 << 16 : tab ? p1 : 0u, t == 3u ? p1 : 0u};
 }
 
+// A span's function with one more event of type t at p1 composed onto it: LCompose(a,
+// ev_fn(t, p1)) with the event's constants folded in (TSV; ~16 VALU instead of ~22).  The
+// halves whose exit mode is V (sel half 0x0302: bit 1 set) take a newline's record end and
+// boundary, the halves in K a TAB's boundary; positions only grow, so the max is the new one.
+template <bool MDBM>
+__device__ inline LFn lfn_push(const LFn& a, uint32_t t, uint32_t p1) {
+  if constexpr (MDBM) return LCompose()(a, ev_fn<MDBM>(t, p1));
+  const uint32_t vm = (a.sel >> 1) & 0x00010001u;  // 1 per half in V
+  const uint32_t hm = vm * 0xFFFFu;                // 0xFFFF per half in V
+  const bool nl = t == 1u, tab = t == 2u;
+  const uint32_t take = nl ? hm : tab ? ~hm : 0u;
+  return LFn{nl ? (kSelK | (kSelK << 16)) : tab ? (kSelV | (kSelV << 16)) : a.sel, a.cnt + (nl ? vm : 0u),
+             (a.last & ~take) | ((p1 | (p1 << 16)) & take), t == 3u ? p1 : a.c};
+}
+
 // Walk the candidate bytes of a span staged at `span`, calling f(offset, type) for each
 // (type 0 for a candidate that is no event: f must treat it as none).
 template <bool MDBM, class F>
@@ -325,7 +381,7 @@ __device__ inline void span_events(const uint8_t* span, F&& f) {
   uint32_t o = next_event(mm[0], mm[1]), c = span[o & 127u];
   while (o < 128) {
     const uint32_t on = next_event(mm[0], mm[1]), cn = span[on & 127u];
-    f(o, ev_type<MDBM>(c));
+    f(o, cand_type<MDBM>(c));
     o = on;
     c = cn;
   }
@@ -355,12 +411,15 @@ __device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, con
 // exactly after every newline the value getline reads, and ends at the first TAB or NUL
 // after it (the key getline's TAB, or the C-string cut).  So for every cut event (TAB /
 // NUL) that is the first after a newline of the same block, pass A hashes the bytes
-// between them and appends the raw state with the key's start to the block's list; the
-// j-th cut event of a span (j < kSlots) keeps the list index in its packed word.
-// Pass B, whose walk ends a key at cut event j of its span, takes the slot when the key's
-// true start equals the stored one; every other key (the file's first, a key whose newline
-// is in an earlier block, a third cut in one span, a span with more than kEvCap events)
-// is hashed from the file.
+// between them: the j-th cut event of a span (j < kSlots) keeps the key's length in its
+// packed word and the raw state in the span's slot j (SpecSlots).  Pass B, whose walk ends
+// a key at cut event j of its span, takes the slot when the key's true length equals the
+// stored one (same end, same length: the same bytes); every other key (the file's first,
+// a key whose newline is in an earlier block, a third cut in one span, a span with more
+// than kEvCap events, a key of 255 bytes or more) is hashed from the file.
+// Round 4: slots indexed by span, so pass B loads its states with its packed word instead
+// of after it (round 3: a per-block list indexed from the packed word, 10 B per key -- a
+// second dependent HBM round trip at the start of every pass-B wave).
 constexpr uint32_t kSlots = 2;
 // The head key: the key that ends at a block's first cut event when no newline precedes it
 // in the block started in the bytes before the block (a key straddling the boundary, ~1 in
@@ -371,11 +430,11 @@ constexpr uint32_t kSlots = 2;
 // at the file's first byte.
 constexpr uint32_t kPre = 256;
 constexpr uint32_t kListCap = 160;  // keys hashed by pass A per block (BASELINE-like files: ~120; < 0xFF)
-// A block's list is two arrays at the same index: the FNV state after the key's bytes (h2
-// of key + NUL; h1 = raw * P) and the key's block-relative start (10 bytes per key).
-struct SpecList {
-  uint64_t* raw;     // [nblk * kListCap]
-  uint16_t* start;   // [nblk * kListCap]
+constexpr uint32_t kSpecLenMax = 254;  // longest key a slot holds (0xFF: no slot)
+// Each span's slots: the FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
+// at raw[kSlots * span + j], written only for the slots its packed word names.
+struct SpecSlots {
+  uint64_t* raw;  // [nblk * kTThreads * kSlots]
 };
 
 // Newline state of a span for the speculative keys: whether it holds a newline, whether
@@ -472,7 +531,7 @@ __device__ inline GFn block_scan_runs(Tmp& tmp, In&& in, uint64_t n, uint64_t k,
 template <bool MDBM>
 __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                           GFn* __restrict__ blk_fn, uint64_t* __restrict__ ev,
-                                                          SpecList spec, SpadTable sp) {
+                                                          SpecSlots spec, SpadTable sp) {
   constexpr uint32_t PRE = MDBM ? 0u : kPre;
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + PRE + kTChunk];
   // emitted keys: start (16-bit, signed) | len << 16 (32 bits: the block's LDS must stay
@@ -483,6 +542,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __shared__ uint32_t s_cls[8];        // keys per chunk-count class, then class offsets
   __shared__ typename hipcub::WarpReduce<LFn, 64>::TempStorage s_wred[kTThreads / 64];
   __shared__ uint8_t s_ord[kListCap];  // list indices in class order
+  __shared__ uint8_t s_slot[kListCap];  // each listed key's span (in the block) * kSlots + cut index
   typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
   __shared__ typename NlScan::TempStorage tmp;
   if (threadIdx.x == 0) s_nk = 0;
@@ -498,7 +558,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
   if (live)
     span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
-      acc = LCompose()(acc, ev_fn<MDBM>(t, rel + o + 1));
+      acc = lfn_push<MDBM>(acc, t, rel + o + 1);
       const uint64_t e = (uint64_t)(o | (t << 7)) << (9 * min(ne, kEvCap - 1));
       pk |= (t && ne < kEvCap) ? e : 0ull;
       ne += t ? 1u : 0u;
@@ -548,10 +608,12 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
             }
           }
         }
-        const uint32_t slot = ok ? atomicAdd(&s_nk, 1u) : kListCap;
+        const uint32_t len = (uint32_t)((int32_t)pos - start);
+        const uint32_t slot = ok && len <= kSpecLenMax ? atomicAdd(&s_nk, 1u) : kListCap;
         if (slot < kListCap) {
-          s_key[slot] = ((uint32_t)start & 0xFFFFu) | ((uint32_t)((int32_t)pos - start) << 16);
-          pk = (pk & ~(0xFFull << (48 + 8 * j))) | ((uint64_t)slot << (48 + 8 * j));
+          s_key[slot] = ((uint32_t)start & 0xFFFFu) | (len << 16);
+          s_slot[slot] = (uint8_t)(kSlots * threadIdx.x + j);
+          pk = (pk & ~(0xFFull << (48 + 8 * j))) | ((uint64_t)len << (48 + 8 * j));
         }
       }
       open = false;
@@ -591,14 +653,33 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     if (i < nk) s_ord[atomicAdd(&s_cls[cls[h]], 1u)] = (uint8_t)i;
   }
   __syncthreads();
-  for (uint32_t q = threadIdx.x; q < nk; q += kTThreads) {
-    const uint32_t i = s_ord[q];
-    const uint32_t k = s_key[i];
-    const int32_t st = (int16_t)(k & 0xFFFFu);
-    const uint32_t len = k >> 16;
-    spec.raw[(uint64_t)blockIdx.x * kListCap + i] = key_raw_lds(blk + 16 + st, len, sp);
-    spec.start[(uint64_t)blockIdx.x * kListCap + i] = (uint16_t)(k & 0xFFFFu);
+  uint64_t raw[2];
+  uint32_t slot[2];
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h) {
+    const uint32_t q = threadIdx.x + h * kTThreads;
+    slot[h] = 0xFFFFFFFFu;
+    if (q < nk) {
+      const uint32_t i = s_ord[q];
+      const uint32_t k = s_key[i];
+      raw[h] = key_raw_lds(blk + 16 + (int16_t)(k & 0xFFFFu), k >> 16, sp);
+      slot[h] = s_slot[i];
+    }
   }
+  // The states go out as one 16-byte store per span (both slots; a slot no key took holds
+  // whatever the LDS held): through the staged block's LDS, free once every key is hashed.
+  // (Stored where they were hashed, 8 bytes at a time into the sparse slot array, they
+  // cost pass A +14 us: partial-line writes.)
+  __syncthreads();
+  uint64_t* s_raw = reinterpret_cast<uint64_t*>(lds);  // [kTThreads * kSlots]
+#pragma unroll
+  for (uint32_t h = 0; h < 2; ++h)
+    if (slot[h] != 0xFFFFFFFFu) s_raw[slot[h]] = raw[h];
+  __syncthreads();
+  typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
+  static_assert(kSlots == 2, "one 16-byte store per span");
+  *reinterpret_cast<u64x2a*>(spec.raw + (uint64_t)blockIdx.x * (kTThreads * kSlots) + kSlots * threadIdx.x) =
+      *reinterpret_cast<const u64x2a*>(s_raw + kSlots * threadIdx.x);
 }
 
 // The entry-state scan between the passes, one block per tile: the tile's functions into
@@ -664,7 +745,6 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
                                                           const TState* __restrict__ tile_in,
                                                           const uint64_t* __restrict__ ev,
                                                           const uint64_t* __restrict__ spec_raw,
-                                                          const uint16_t* __restrict__ spec_start,
                                                           const uint64_t* __restrict__ count, uint64_t cap,
                                                           k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
                                                           uint64_t* __restrict__ h1, uint64_t* __restrict__ h2,
@@ -674,7 +754,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   __shared__ typename Scan::TempStorage tmp;
   constexpr uint64_t HDR = MDBM ? kHdrRecs : 0;
   const uint64_t base = (uint64_t)blockIdx.x * kUnit;
-  const uint64_t blk = blockIdx.x / kUnitsPerBlock, blk_base = blk * kTChunk;  // pass A's block (spec list)
+  const uint64_t blk = blockIdx.x / kUnitsPerBlock;  // pass A's block
   const uint32_t rel = kTBytes * threadIdx.x;
   const bool live = base + rel < size;
   const uint64_t ti = base / kTBytes + threadIdx.x;
@@ -682,49 +762,34 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   const GFn ein = intile[blockIdx.x];
   const TState tin = tile_in[blk / kTile];
   const bool over = ev_count(pk) == 7u;
-  // the slots pass A wrote for this span, loaded now so their latency hides under the scan
-  uint64_t sl_raw[kSlots];
-  uint32_t sl_start[kSlots];
-#pragma unroll
-  for (uint32_t j = 0; j < kSlots; ++j) {
-    sl_raw[j] = 0;
-    sl_start[j] = 0xFFFFFFFFu;
-    const uint32_t li = (uint32_t)(pk >> (48 + 8 * j)) & 0xFFu;
-    if (HASH && !MDBM && li != 0xFFu) {
-      sl_raw[j] = spec_raw[blk * kListCap + li];
-      sl_start[j] = spec_start[blk * kListCap + li];
-    }
-  }
+  // the span's slots, loaded with its packed word (a slot pass A did not write holds a
+  // stale state, used only when the packed word names it)
+  static_assert(kSlots == 2, "one 16-byte load per span");
+  typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
+  u64x2a sl_raw = u64x2a{0, 0};
+  if (HASH && !MDBM && live) sl_raw = *reinterpret_cast<const u64x2a*>(spec_raw + kSlots * ti);
   // a span with more than kEvCap events (rare): its candidate masks from the file, each
   // candidate's byte read back (no LDS, so the kernel keeps its occupancy)
   uint64_t om0 = 0, om1 = 0;
   if (over && live) {
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    uint32_t nib[4] = {0, 0, 0, 0};
+    uint32_t w[32];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      uint32_t w[4];
       const uint64_t o = base + rel + 16ull * q;
       if (o + 16 <= size && (((uintptr_t)(f + o)) & 15) == 0) {
         const u32x4 v = *reinterpret_cast<const u32x4*>(f + o);
-        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+        w[4 * q] = v.x, w[4 * q + 1] = v.y, w[4 * q + 2] = v.z, w[4 * q + 3] = v.w;
       } else {
         for (int k = 0; k < 4; ++k) {
-          w[k] = 0x01010101u;
+          uint32_t x = 0x01010101u;
           for (int b = 0; b < 4; ++b)
-            if (o + 4 * k + b < size) w[k] = (w[k] & ~(0xFFu << (8 * b))) | ((uint32_t)f[o + 4 * k + b] << (8 * b));
+            if (o + 4 * k + b < size) x = (x & ~(0xFFu << (8 * b))) | ((uint32_t)f[o + 4 * k + b] << (8 * b));
+          w[4 * q + k] = x;
         }
       }
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const uint32_t small = ~(((w[k] & 0x7F7F7F7Fu) + 0x75757575u) | w[k]) & 0x80808080u;  // bytes < 0x0B
-        const uint32_t n4 = (small * 0x00204081u) >> 28;
-        const int word = 4 * q + k;
-        nib[word >> 3] |= n4 << (4 * (word & 7));
-      }
     }
-    om0 = nib[0] | ((uint64_t)nib[1] << 32);
-    om1 = nib[2] | ((uint64_t)nib[3] << 32);
+    cand_masks(w, om0, om1);
   }
   auto for_events = [&](auto&& fn) {
     if (!live) return;
@@ -743,7 +808,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     }
   };
   LFn acc = lfn_id();
-  for_events([&](uint32_t o, uint32_t t) { acc = LCompose()(acc, ev_fn<MDBM>(t, rel + o + 1)); });
+  for_events([&](uint32_t o, uint32_t t) { acc = lfn_push<MDBM>(acc, t, rel + o + 1); });
   LFn pre;
   Scan(tmp).ExclusiveScan(acc, pre, lfn_id(), LCompose());
   TState s = gapply(gfn_of(pre, base), gapply(ein, tin));
@@ -767,17 +832,10 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     pk_len = e - s.fs;
     if constexpr (HASH) {
       uint64_t a, c;
-      // the key's start relative to the block as pass A stored it (16 bits; a key that
-      // starts in the bytes before the block, pass A's head key, is negative)
-      const uint32_t want = s.fs + kTChunk >= blk_base ? (uint32_t)((s.fs - blk_base) & 0xFFFFu) : 0xFFFFFFFEu;
-      bool hit = false;
-      uint64_t raw = 0;
-#pragma unroll
-      for (uint32_t q = 0; q < kSlots; ++q)
-        if (j == q && sl_start[q] == want) {
-          hit = true;
-          raw = sl_raw[q];
-        }
+      // pass A's key for this cut event, if its length is this key's (0xFF: none)
+      const uint64_t len = e - s.fs;
+      const bool hit = j < kSlots && len <= kSpecLenMax && ((pk >> (48 + 8 * j)) & 0xFFu) == len;
+      const uint64_t raw = j == 0 ? sl_raw.x : sl_raw.y;
       if (hit) {
         a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
         c = e > s.fs ? raw : a;
@@ -866,7 +924,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
 // The entry-state scan's counter lives in a second buffer that is never freed: it must be
 // zero at every call (the scan leaves it zero), so it is cleared only when allocated.
 // The record count and the mdbm flags come back through mapped pinned host memory.
-constexpr uint64_t kScratchKeep = 512ull << 20;  // > the temporaries of a 1.2 GB TSV file (~23 % of its size)
+constexpr uint64_t kScratchKeep = 512ull << 20;  // > the temporaries of a 1.2 GB TSV file (~20 % of its size)
 struct ScanScratch {
   std::mutex mu;
   void* p = nullptr;
@@ -882,7 +940,7 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 // TSV and mdbm: pass A, the scan of block functions (and the count), pass B (mdbm always:
 // it checks the header; TSV when records are wanted), one synchronisation.  Temporaries per
 // 16 KiB block: its function and in-tile prefix (2 x 48 B), 8 B of events per 128 B span,
-// and the block's list of speculative key states (TSV: 10 B each, up to kListCap); per tile
+// and two speculative key states per span (TSV: 16 B per 128 B span); per tile
 // of kTile blocks its function and entry state.
 template <bool MDBM>
 static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs, uint64_t cap, uint64_t* count,
@@ -904,9 +962,9 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
   const size_t nfn = nblk * kUnitsPerBlock;  // pass A writes every wave's function, past-EOF ones too
   const size_t o_fn = 0, o_in = o_fn + align256(nfn * sizeof(GFn)), o_tf = o_in + align256(nfn * sizeof(GFn));
   const size_t o_ti = o_tf + align256(ntile * sizeof(GFn)), o_ev = o_ti + align256(ntile * sizeof(TState));
-  const size_t nspec = MDBM ? 0 : nblk * kListCap;
-  const size_t o_spec = o_ev + align256(nblk * kTThreads * 8), o_start = o_spec + align256(nspec * 8);
-  const size_t total = o_start + align256(nspec * 2);
+  const size_t nspec = MDBM ? 0 : nblk * kTThreads * kSlots;
+  const size_t o_spec = o_ev + align256(nblk * kTThreads * 8);
+  const size_t total = o_spec + align256(nspec * 8);
   ScanScratch& sc = g_scan[dev];
   std::lock_guard<std::mutex> lk(sc.mu);
   if (e == hipSuccess && sc.bytes < total) {
@@ -955,7 +1013,7 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
   es.mdbm = MDBM ? 1u : 0u;
   uint64_t* dcount = es.count;
   uint64_t* ev = (uint64_t*)(base + o_ev);
-  const SpecList spec{(uint64_t*)(base + o_spec), (uint16_t*)(base + o_start)};
+  const SpecSlots spec{(uint64_t*)(base + o_spec)};
   const bool walk = MDBM || (recs && cap);
   const uint64_t wcap = recs ? cap : 0;
   const SpadTable sp = make_spad(seed);
@@ -968,10 +1026,10 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
   if (e == hipSuccess && walk) {
     if (h1 && recs)
       tsv_b_kernel<true, MDBM><<<(unsigned)nunit, 64, 0, stream>>>(
-          f, size, es.intile, es.tile_in, ev, spec.raw, spec.start, dcount, wcap, recs, sp, h1, h2, sc.hflags_d);
+          f, size, es.intile, es.tile_in, ev, spec.raw, dcount, wcap, recs, sp, h1, h2, sc.hflags_d);
     else
       tsv_b_kernel<false, MDBM><<<(unsigned)nunit, 64, 0, stream>>>(
-          f, size, es.intile, es.tile_in, ev, spec.raw, spec.start, dcount, wcap, recs, sp, nullptr, nullptr,
+          f, size, es.intile, es.tile_in, ev, spec.raw, dcount, wcap, recs, sp, nullptr, nullptr,
           sc.hflags_d);
     tr(hipGetLastError());
   }

@@ -38,11 +38,14 @@ def main():
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--ab", default="", help="another build of libk2hash_amd.so to time against the tree's")
     ap.add_argument("--rounds", type=int, default=9)
+    ap.add_argument("--lib", default="", help="run (and profile) this build instead of the tree's")
     ap.add_argument("--no-parity", action="store_true", help="probe libraries (tools/probe_build.py): time without "
                     "the digest check (their results may be wrong by design)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     data = bench.import_workload(dev)
+    if a.lib:
+        _native._batch = _native._bind(ctypes.CDLL(str(Path(a.lib).resolve())), _native.SIGNATURES.keys())
     if a.ab:
         libs = {"tree": _native.batch_lib()}
         for p in a.ab.split(","):
