@@ -18,6 +18,7 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 
 #include "../../include/k2hash_amd.h"
@@ -545,17 +546,26 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __shared__ uint8_t s_slot[kListCap];  // each listed key's span (in the block) * kSlots + cut index
   typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
   __shared__ typename NlScan::TempStorage tmp;
+  uint8_t* blk = lds + PRE;  // block byte i at blk[16 + i]; the kPre bytes before the block below it
+  const uint64_t bid = blockIdx.x;
   if (threadIdx.x == 0) s_nk = 0;
   if (threadIdx.x < 8) s_cls[threadIdx.x] = 0;
-  const uint64_t base = (uint64_t)blockIdx.x * kTChunk;
-  uint8_t* blk = lds + PRE;  // block byte i at blk[16 + i]; the kPre bytes before the block below it
-  tsv_stage<PRE>(f, size, blockIdx.x, lds);  // (its barrier publishes s_nk = 0)
+  const uint64_t base = bid * kTChunk;
+  tsv_stage<PRE>(f, size, bid, lds);  // (its barrier publishes s_nk = 0)
   const uint32_t rel = kTBytes * threadIdx.x;
   const uint8_t* span = blk + 16 + rel;
   const bool live = base + rel < size;
   LFn acc = lfn_id();
-  uint64_t pk = 0;
+  uint64_t pk = kNoSlots;
   uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
+  // Speculative keys, found in the same walk (round 4; round 3 walked the packed events a
+  // second time after the block scan): a cut that follows a newline of this span ends the
+  // key that starts after it; the span's first cut, if no newline precedes it here, waits
+  // for the scan (cut0) -- the entering state decides whether it ends a key, and where
+  // that key starts.
+  uint32_t j = 0;                     // cut events so far
+  int32_t lnl = -1;                   // the last newline's position in the block while no cut followed it
+  uint32_t cut0 = 0xFFFFFFFFu;        // the span's first cut when no newline precedes it
   if (live)
     span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
       acc = lfn_push<MDBM>(acc, t, rel + o + 1);
@@ -563,64 +573,68 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
       pk |= (t && ne < kEvCap) ? e : 0ull;
       ne += t ? 1u : 0u;
       nl = t == 1u ? (1u | 2u | ((rel + o) << 2)) : t ? (nl & ~2u) : nl;
+      if constexpr (!MDBM) {
+        const bool cut = t >= 2u;  // TAB or NUL
+        if (cut && j == 0 && lnl < 0 && !(nl & 1u)) cut0 = rel + o;
+        const uint32_t len = rel + o - (uint32_t)(lnl + 1);
+        if (cut && j < kSlots && lnl >= 0 && len <= kSpecLenMax) {
+          const uint32_t slot = atomicAdd(&s_nk, 1u);
+          if (slot < kListCap) {
+            s_key[slot] = ((uint32_t)(lnl + 1) & 0xFFFFu) | (len << 16);
+            s_slot[slot] = (uint8_t)(kSlots * threadIdx.x + j);
+            const uint32_t sh = j ? 56u : 48u;
+            pk = (pk & ~(0xFFull << sh)) | ((uint64_t)len << sh);
+          }
+        }
+        lnl = cut ? -1 : t == 1u ? (int32_t)(rel + o) : lnl;
+        j += cut ? 1u : 0u;
+      }
     });
   const bool over = ne > kEvCap;
-  pk = over ? kEvOverflow : pk | ((uint64_t)ne << 45) | kNoSlots;
   const LFn wf = wave_fn_reduce(s_wred[threadIdx.x >> 6], acc);
-  if ((threadIdx.x & 63u) == 0) blk_fn[(uint64_t)blockIdx.x * kUnitsPerBlock + (threadIdx.x >> 6)] = gfn_of(wf, base);
+  if ((threadIdx.x & 63u) == 0) blk_fn[bid * kUnitsPerBlock + (threadIdx.x >> 6)] = gfn_of(wf, base);
   if constexpr (MDBM) {
-    ev[base / kTBytes + threadIdx.x] = pk;
+    ev[base / kTBytes + threadIdx.x] = over ? kEvOverflow : pk | ((uint64_t)ne << 45);
     return;
   }
   uint32_t pre_nl;
   NlScan(tmp).ExclusiveScan(live ? nl : 2u, pre_nl, 2u, NlOp());
-  // keys ending at this span's cuts: the newline state entering the span, then its events;
-  // each key goes to the block's list, hashed below one lane per key.  head: no newline and
-  // no cut before this span in the block, so its first cut may end the head key.
-  bool open = (pre_nl & 3u) == 3u, head = pre_nl == 2u;
-  int32_t start = (int32_t)(pre_nl >> 2) + 1;
-  uint32_t j = 0;
-  if (live && !over) {
-    for (uint32_t q = 0; q < ne; ++q) {
-      const uint32_t e = (uint32_t)(pk >> (9 * q)) & 0x1FFu;
-      const uint32_t pos = rel + (e & 127u), t = e >> 7;
-      if (t == 1u) {
-        open = true;
-        head = false;
-        start = (int32_t)pos + 1;
-        continue;
-      }
-      if ((open || head) && j < kSlots && base + pos < size) {  // the first cut after a newline
-        bool ok = true;
-        if (head) {  // the byte after the last newline of the prefix (block 0: the file's first)
-          ok = base == 0;
-          start = 0;
-          for (int32_t w = (int32_t)PRE / 16 - 1; w >= 0 && !ok; --w) {
-            const uint4 c = ld16(lds + 16 + 16 * w);
-            const uint32_t wd[4] = {c.x, c.y, c.z, c.w};
-            for (int32_t k = 3; k >= 0 && !ok; --k) {
-              const uint32_t x = wd[k] ^ 0x0A0A0A0Au;
-              const uint32_t m = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // bit 7 of 0x0A bytes
-              if (m) {
-                start = 16 * w + 4 * k + (31 - (int32_t)__clz(m)) / 8 + 1 - (int32_t)PRE;
-                ok = true;
-              }
-            }
+  // cut0 ends a key if the state entering the span is a newline with no cut after it
+  // (open), or if nothing precedes the span in the block (head: the key started before the
+  // block, after the last newline of the kPre bytes before it; block 0: at the file's start)
+  const bool open = (pre_nl & 3u) == 3u, head = pre_nl == 2u;
+  if (cut0 != 0xFFFFFFFFu && (open || head)) {
+    bool ok = true;
+    int32_t start = (int32_t)(pre_nl >> 2) + 1;
+    if (head) {
+      ok = base == 0;
+      start = 0;
+      for (int32_t w = (int32_t)PRE / 16 - 1; w >= 0 && !ok; --w) {
+        const uint4 c = ld16(lds + 16 + 16 * w);
+        const uint32_t wd[4] = {c.x, c.y, c.z, c.w};
+        for (int32_t k = 3; k >= 0 && !ok; --k) {
+          const uint32_t x = wd[k] ^ 0x0A0A0A0Au;
+          const uint32_t m = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);  // bit 7 of 0x0A bytes
+          if (m) {
+            start = 16 * w + 4 * k + (31 - (int32_t)__clz(m)) / 8 + 1 - (int32_t)PRE;
+            ok = true;
           }
         }
-        const uint32_t len = (uint32_t)((int32_t)pos - start);
-        const uint32_t slot = ok && len <= kSpecLenMax ? atomicAdd(&s_nk, 1u) : kListCap;
-        if (slot < kListCap) {
-          s_key[slot] = ((uint32_t)start & 0xFFFFu) | (len << 16);
-          s_slot[slot] = (uint8_t)(kSlots * threadIdx.x + j);
-          pk = (pk & ~(0xFFull << (48 + 8 * j))) | ((uint64_t)len << (48 + 8 * j));
-        }
       }
-      open = false;
-      head = false;
-      ++j;
+    }
+    const uint32_t len = (uint32_t)((int32_t)cut0 - start);
+    if (ok && len <= kSpecLenMax) {
+      const uint32_t slot = atomicAdd(&s_nk, 1u);
+      if (slot < kListCap) {
+        s_key[slot] = ((uint32_t)start & 0xFFFFu) | (len << 16);
+        s_slot[slot] = (uint8_t)(kSlots * threadIdx.x);
+        pk = (pk & ~(0xFFull << 48)) | ((uint64_t)len << 48);
+      }
     }
   }
+  // a span with more than kEvCap events keeps its slots: pass B re-reads its events from
+  // the file and counts its cuts the same way
+  pk = over ? (kEvOverflow & ~kNoSlots) | (pk & kNoSlots) : pk | ((uint64_t)ne << 45);
   ev[base / kTBytes + threadIdx.x] = pk;
   __syncthreads();
   // The list's keys in order of chunk count (counting sort over 8 classes), so that each
@@ -678,7 +692,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __syncthreads();
   typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
   static_assert(kSlots == 2, "one 16-byte store per span");
-  *reinterpret_cast<u64x2a*>(spec.raw + (uint64_t)blockIdx.x * (kTThreads * kSlots) + kSlots * threadIdx.x) =
+  *reinterpret_cast<u64x2a*>(spec.raw + bid * (kTThreads * kSlots) + kSlots * threadIdx.x) =
       *reinterpret_cast<const u64x2a*>(s_raw + kSlots * threadIdx.x);
 }
 
