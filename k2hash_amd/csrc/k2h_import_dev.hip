@@ -879,36 +879,26 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       *reinterpret_cast<u64x2*>(&recs[r].val_off) = u64x2{s.fs, e - s.fs};
     }
   };
+  // The walk, one branch per event (round 4; round 3 branched on the event type and the mode,
+  // ~60 SALU per event for the exec-mask bookkeeping): which field's C string ends here,
+  // then the state by selects.  A field ends at its getline's delimiter (TSV: TAB for a
+  // key, newline for a value; mdbm: newline for both) or at its first NUL; the delimiter
+  // flips the mode, and a newline read in V ends the record.
   for_events([&](uint32_t o, uint32_t t) {
     const uint64_t pos = base + rel + o;
-    if (t == 1u) {
-      if (s.m) {  // the value getline's newline: the record ends
-        if (!nulf) val_end(pos, false);
-        s.m = 0;
-        ++s.r;
-        s.fs = pos + 1;
-        nulf = false;
-      } else if (MDBM) {  // mdbm: the key line's newline
-        if (!nulf) key_end(pos);
-        s.m = 1;
-        s.fs = pos + 1;
-        nulf = false;
-      }
-      return;
+    const bool nl = t == 1u, nul = t == 3u;
+    const bool brk = MDBM ? nl : (s.m ? nl : t == 2u);  // the getline's delimiter
+    if (!nulf && (brk || nul)) {
+      if (s.m)
+        val_end(pos, nul);
+      else
+        key_end(pos);
     }
-    if (t == 2u) {
-      if (!s.m) {  // the key getline's TAB
-        if (!nulf) key_end(pos);
-        s.m = 1;
-        s.fs = pos + 1;
-        nulf = false;
-      }
-    } else if (!nulf) {  // the field's first NUL: its C string ends here
-      if (s.m) val_end(pos, true);
-      else key_end(pos);
-      nulf = true;
-    }
-    ++j;
+    s.r += (nl && s.m) ? 1u : 0u;
+    s.fs = brk ? pos + 1 : s.fs;
+    nulf = !brk && (nulf || nul);
+    s.m = brk ? s.m ^ 1u : s.m;
+    j += nl ? 0u : 1u;  // cut events: TAB and NUL
   });
   if (live && base + rel + kTBytes >= size) {  // the thread holding the last byte
     if (s.m && !nulf) val_end(size, false);    // a value read to EOF
