@@ -489,6 +489,7 @@ struct EntryScan {
 // the header starts record kHdrRecs -- real record r is machine record r + kHdrRecs.  The
 // fifth header line is record 2's value line (checked in pass B).
 constexpr uint64_t kHdrRecs = 3;
+constexpr uint32_t kStageRecs = 96;  // records a pass-B unit stages in LDS (BASELINE-like files: ~60 per 8 KiB)
 
 // Exclusive scan of in(0) .. in(n - 1) by one block, thread t owning the run [t k, (t + 1) k):
 // out(i, prefix of in(0 .. i - 1)); returns the whole reduction.  Runs of up to 4 are loaded
@@ -766,6 +767,12 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   // one wave per 8 KiB unit: the span functions' prefix is a wave scan (no LDS, no barrier)
   typedef hipcub::WarpScan<LFn, 64> Scan;
   __shared__ typename Scan::TempStorage tmp;
+  // The unit's records, staged in LDS and written out as consecutive 16-byte pieces across
+  // the wave (round 4; round 3: each lane stored its own records' halves, 1.31x the
+  // algorithmic bytes written).  A unit with more than kStageRecs records stores directly.
+  __shared__ uint64_t s_rec[kStageRecs * 4];  // key_off, key_len, val_off, val_len
+  __shared__ uint64_t s_h[kStageRecs * 2];    // h1, h2
+  __shared__ uint8_t s_fk[kStageRecs], s_fv[kStageRecs], s_fh[kStageRecs];  // which parts this unit wrote
   constexpr uint64_t HDR = MDBM ? kHdrRecs : 0;
   const uint64_t base = (uint64_t)blockIdx.x * kUnit;
   const uint64_t blk = blockIdx.x / kUnitsPerBlock;  // pass A's block
@@ -823,10 +830,17 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   };
   LFn acc = lfn_id();
   for_events([&](uint32_t o, uint32_t t) { acc = lfn_push<MDBM>(acc, t, rel + o + 1); });
-  LFn pre;
-  Scan(tmp).ExclusiveScan(acc, pre, lfn_id(), LCompose());
-  TState s = gapply(gfn_of(pre, base), gapply(ein, tin));
+  LFn pre, agg;
+  Scan(tmp).ExclusiveScan(acc, pre, lfn_id(), LCompose(), agg);
+  const TState su = gapply(ein, tin);  // the state entering the unit
+  TState s = gapply(gfn_of(pre, base), su);
   const uint64_t lim = min(count[0], cap) + HDR;  // machine record indices below lim are written
+  // the unit touches records su.r .. su.r + (its record ends), the last one possibly in part
+  const uint32_t nrec = (su.m ? agg.cnt >> 16 : agg.cnt & 0xFFFFu) + 1u;
+  const bool staged = nrec <= kStageRecs;
+  if (staged)
+    for (uint32_t q = threadIdx.x; q < nrec; q += 64) s_fk[q] = s_fv[q] = s_fh[q] = 0;
+  __syncthreads();
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
   uint32_t j = 0;           // cut events of this span so far
   // a key ended in this span whose record's value has not ended yet: its fields wait so
@@ -840,10 +854,17 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   auto key_end = [&](uint64_t e) {
     if (s.r < HDR || s.r >= lim) return;
     const uint64_t r = s.r - HDR;
-    flush_key();
-    pk_r = r;
-    pk_off = s.fs;
-    pk_len = e - s.fs;
+    const uint32_t x = (uint32_t)(s.r - su.r);  // staged: its index in the unit
+    if (staged) {
+      s_rec[4 * x] = s.fs;
+      s_rec[4 * x + 1] = e - s.fs;
+      s_fk[x] = 1;
+    } else {
+      flush_key();
+      pk_r = r;
+      pk_off = s.fs;
+      pk_len = e - s.fs;
+    }
     if constexpr (HASH) {
       uint64_t a, c;
       // pass A's key for this cut event, if its length is this key's (0xFF: none)
@@ -856,8 +877,14 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       } else {
         hash_cstr(f, s.fs, e - s.fs, sp, a, c);
       }
-      h1[r] = a;
-      if (h2) h2[r] = c;
+      if (staged) {
+        s_h[2 * x] = a;
+        s_h[2 * x + 1] = c;
+        s_fh[x] = 1;
+      } else {
+        h1[r] = a;
+        if (h2) h2[r] = c;
+      }
     }
   };
   auto val_end = [&](uint64_t e, bool at_nul) {
@@ -871,7 +898,12 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     }
     if (s.r < HDR || s.r >= lim) return;
     const uint64_t r = s.r - HDR;
-    if (pk_r == r) {
+    if (staged) {
+      const uint32_t x = (uint32_t)(s.r - su.r);
+      s_rec[4 * x + 2] = s.fs;
+      s_rec[4 * x + 3] = e - s.fs;
+      s_fv[x] = 1;
+    } else if (pk_r == r) {
       *reinterpret_cast<u64x2*>(&recs[r].key_off) = u64x2{pk_off, pk_len};
       *reinterpret_cast<u64x2*>(&recs[r].val_off) = u64x2{s.fs, e - s.fs};
       pk_r = ~0ull;
@@ -906,8 +938,14 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       if (!s.m && s.fs < size) {  // a key line at EOF: the key, and the previous record's value
         if (!nulf) key_end(size);
         if (s.r >= HDR && s.r < lim) {
-          if (s.r == HDR)
+          if (s.r == HDR && staged) {
+            const uint32_t x = (uint32_t)(s.r - su.r);
+            s_rec[4 * x + 2] = s.fs;
+            s_rec[4 * x + 3] = 0;
+            s_fv[x] = 1;
+          } else if (s.r == HDR) {
             *reinterpret_cast<u64x2*>(&recs[0].val_off) = u64x2{s.fs, 0ull};
+          }
           else
             __hip_atomic_store(hflags + 2, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -915,6 +953,21 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     }
   }
   flush_key();
+  if (!staged) return;
+  __syncthreads();
+  // the staged parts, consecutive lanes on consecutive 16-byte pieces (a record's key half
+  // or value half that another unit writes is skipped)
+  for (uint32_t q = threadIdx.x; q < 2 * nrec; q += 64) {
+    const uint32_t x = q >> 1, half = q & 1u;
+    if (half ? s_fv[x] : s_fk[x])
+      *reinterpret_cast<u64x2*>(&recs[su.r + x - HDR].key_off + 2 * half) = u64x2{s_rec[2 * q], s_rec[2 * q + 1]};
+  }
+  if constexpr (HASH)
+    for (uint32_t x = threadIdx.x; x < nrec; x += 64)
+      if (s_fh[x]) {
+        h1[su.r + x - HDR] = s_h[2 * x];
+        if (h2) h2[su.r + x - HDR] = s_h[2 * x + 1];
+      }
 }
 
 }  // namespace

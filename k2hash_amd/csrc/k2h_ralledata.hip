@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
       dst[u] = kGatherHdr + 80 * R + 16 * (uint32_t)q;
     }
   }
-  // 1b. one thread per record: header, segment table, piece table, blob offset.  All
+  // 1b. one thread per record: header, segment table.  All
   // block-relative quantities fit 32 bits once the spans fit the image.
   const uint64_t a_out = (uint64_t)(uintptr_t)(out + o_first);
   const int32_t d0 = (int32_t)(a_out & 15u);
@@ -282,17 +282,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
     for (int c = 0; c < 5; ++c)
       *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid + 16 * c) = u32x4_al{f[4 * c], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]};
     int32_t start = B;
-    int32_t p = tid == 0 ? 0 : (B + d0 + 15) >> 4;  // first piece whose first byte is in this record
 #pragma unroll
     for (int c = 0; c < 5; ++c) {
       const uint32_t g = 5 * tid + c;
       const int32_t L = c == 0 ? 80 : (int32_t)len[c - 1];
       const int32_t adj = c == 0 ? kGatherHdr + 80 * (int32_t)tid - start : area[c - 1] + (int32_t)rel[c - 1] - start;
       seg[g] = seg_pack(adj, start + L);
-      for (; 16 * p - d0 < start + L; ++p) {  // pieces starting in this segment
-        tab[p] = (uint8_t)g;
-        if ((p & 63) == 0) tbase[p >> 6] = (uint16_t)g;
-      }
       start += L;
     }
     if (tid + 1 == nr) seg[5 * nr] = seg_pack(kGatherHdr, start);  // read (never used) as the last segment's successor
@@ -312,6 +307,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
     blob_off[r0 + r] = o_first + (uint64_t)(uint32_t)(seg_unpack(seg[5 * r]).y - 80);
     if (r0 + r + 1 == n) blob_off[n] = o_first + (uint64_t)(uint32_t)seg_unpack(seg[5 * nr]).y;
   }
+  // 1c'. the piece table, by waves 1-3 while wave 0 hashes (round 4: wave 0 built it in 1b,
+  // one divergent loop trip per piece of each of its records' five segments -- ~200 M SALU
+  // per call -- while the other waves waited at the barrier): each segment writes its index
+  // for the pieces whose first byte it holds
+  if (tid >= 64)
+    for (uint32_t g = tid - 64; g < 5 * nr; g += 192) {
+      const int32_t end = seg_unpack(seg[g]).y, beg = g ? seg_unpack(seg[g - 1]).y : 0;
+      for (int32_t p = g ? (beg + d0 + 15) >> 4 : 0; 16 * p - d0 < end; ++p) {
+        tab[p] = (uint8_t)g;
+        if ((p & 63) == 0) tbase[p >> 6] = (uint16_t)g;
+      }
+    }
   // 1c. wave 0 hashes the block's keys from the image into the headers
   if (tid < nr) {
     const uint32_t kl = ro1[0] - ro0[0], ke = ro1[0] - (uint32_t)sbase[0];
