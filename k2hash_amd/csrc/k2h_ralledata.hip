@@ -237,17 +237,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
   constexpr int PPT = (kGatherPool / 16 + NST - 1) / NST;
   u32x4_al v[PPT];
   uint32_t dst[PPT];
+  // (the stream of piece q by selects on 32-bit prefix counts: round 3 tested each stream's
+  // 64-bit range under its own exec mask, ~16 SALU per piece)
+  const uint32_t c1 = (uint32_t)hull_n[0], c2 = c1 + (uint32_t)hull_n[1], c3 = c2 + (uint32_t)hull_n[2];
 #pragma unroll
   for (int u = 0; u < PPT; ++u) {
-    const uint64_t q = (uint64_t)tid - SW + NST * u;
+    const uint32_t q = tid - SW + NST * u;
     dst[u] = 0xffffffffu;
-    if (tid >= SW && q < hull_total) {
-      uint64_t addr = 0, before = 0;
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        if (q >= before && q < before + hull_n[s]) addr = hull_lo[s] + 16 * (q - before);
-        before += hull_n[s];
-      }
+    if (tid >= SW && q < (uint32_t)hull_total) {
+      const bool b1 = q >= c1, b2 = q >= c2, b3 = q >= c3;
+      const uint64_t lo = b3 ? hull_lo[3] : b2 ? hull_lo[2] : b1 ? hull_lo[1] : hull_lo[0];
+      const uint32_t before = b3 ? c3 : b2 ? c2 : b1 ? c1 : 0u;
+      const uint64_t addr = lo + 16ull * (q - before);
       // a global (not flat) load: hipcc must otherwise assume it may touch LDS and makes
       // the LDS reads after the barrier wait for every vector-memory operation
       v[u] = *reinterpret_cast<const __attribute__((address_space(1))) u32x4_al*>((uintptr_t)addr);
