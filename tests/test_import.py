@@ -361,3 +361,35 @@ def test_fused_scan_prehash_many_unspeculated_keys(cuda, oracle):
     assert np.array_equal(h1.cpu().numpy().view(np.uint64), np.array([oracle.k2h_hash(k) for k in keys], np.uint64))
     assert np.array_equal(h2.cpu().numpy().view(np.uint64),
                           np.array([oracle.k2h_second_hash(k) for k in keys], np.uint64))
+
+
+@pytest.mark.gpu
+def test_fused_scan_prehash_staged_and_direct_units(cuda):
+    """Round 4: pass B stages an 8 KiB unit's records in LDS when it touches at most 96 of
+    them and stores directly otherwise.  One file whose units fall on both sides of that
+    line (runs of ~20-byte records: ~400 per unit; ~85-byte records: 95-97 per unit; ~150-byte
+    records), records straddling unit boundaries in every run, keys with NULs: the fused
+    call's records and hashes equal the host scan and the host prehash."""
+    import torch
+    rng = np.random.default_rng(0x5A6E)
+    parts = []
+    for n, klo, khi, vlo, vhi in ((3000, 1, 9, 0, 12), (6000, 8, 40, 55, 63), (4000, 8, 64, 60, 180),
+                                  (3000, 1, 9, 0, 12), (6000, 8, 40, 55, 63)):
+        for _ in range(n):
+            k = bytes(rng.integers(33, 127, int(rng.integers(klo, khi + 1)), dtype=np.uint8))
+            v = bytes(rng.integers(32, 127, int(rng.integers(vlo, vhi + 1)), dtype=np.uint8))
+            if rng.random() < 0.01:
+                k = k[:1] + b"\x00" + k[1:]
+            parts.append(k + b"\t" + v + b"\n")
+    data = b"".join(parts)
+    f = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda)
+    recs, h1, h2 = archive.import_scan_prehash_device(f)
+    torch.cuda.synchronize()
+    host = archive.import_scan(data)
+    a = recs.cpu().numpy().view(np.uint64)
+    assert a.shape[0] == host.size == len(parts)
+    for i, name in enumerate(archive.IMPORT_DTYPE.names):
+        assert np.array_equal(a[:, i], host[name]), name
+    e1, e2 = archive.import_prehash(data, host)
+    assert np.array_equal(h1.cpu().numpy().view(np.uint64), e1)
+    assert np.array_equal(h2.cpu().numpy().view(np.uint64), e2)
