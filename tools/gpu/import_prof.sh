@@ -1,5 +1,5 @@
 #!/bin/bash
-# (round 3 copy of r02ar.sh) import secondary: kernel trace + stats, then FETCH_SIZE / WRITE_SIZE / SQ passes (one group per run)
+# k2himport profile: kernel trace + stats, then FETCH_SIZE / WRITE_SIZE / SQ passes (one group per run)
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
