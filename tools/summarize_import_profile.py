@@ -1,4 +1,4 @@
-"""Summarise tools/gpu/r02ar.sh (rocprofv3 over tools/import_step.py): per call of
+"""Summarise tools/gpu/import_prof.sh (rocprofv3 over tools/import_step.py): per call of
 k2h_amd_import_scan_prehash_device, the kernel time and the PMC counters summed over its
 kernels (tsv_a, tsv_b; round-3 trees before r03i also the block-function scan and
 tsv_count), averaged over the last
@@ -62,7 +62,7 @@ def main():
         "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"), "round": tag, "keys_per_launch": 1 << 23}, indent=1) + "\n")
     s = {"per_kernel_us_per_call": {k: v / 1e3 for k, v in per.items()}, "gpu_us_per_call": gpu_us,
          "pmc_per_call": pmc, "hbm_bytes_per_call": traffic,
-         "source": "tools/gpu/r03_import_prof.sh: rocprofv3 over tools/import_step.py (8M-record TSV, 1.16 GB)"}
+         "source": "tools/gpu/import_prof.sh: rocprofv3 over tools/import_step.py (8M-record TSV, 1.16 GB)"}
     (prof / f"{tag}_import_summary.json").write_text(json.dumps(s, indent=1) + "\n")
     print(json.dumps(s, indent=1))
 
