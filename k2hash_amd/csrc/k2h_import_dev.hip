@@ -430,7 +430,6 @@ constexpr uint32_t kSlots = 2;
 // (~47 us of a 0.62 ms call, profiles/r04d_import_probes.txt).  Block 0's head key starts
 // at the file's first byte.
 constexpr uint32_t kPre = 256;
-constexpr uint32_t kListCap = 160;  // keys hashed by pass A per block (BASELINE-like files: ~120; < 0xFF)
 constexpr uint32_t kSpecLenMax = 254;  // longest key a slot holds (0xFF: no slot)
 // Each span's slots: the FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
 // at raw[kSlots * span + j], written only for the slots its packed word names.
@@ -536,23 +535,22 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
                                                           SpecSlots spec, SpadTable sp) {
   constexpr uint32_t PRE = MDBM ? 0u : kPre;
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + PRE + kTChunk];
-  // emitted keys: start (16-bit, signed) | len << 16 (32 bits: the block's LDS must stay
-  // within 17.5 KiB for 9 blocks per CU -- 18 KiB, one 512-byte granule more, gave 8 and
-  // cost pass A 11 %, round 4)
-  __shared__ uint32_t s_key[kListCap];
-  __shared__ uint32_t s_nk;
+  // The block's speculative keys in chunk-count order, one word each: start (16 bits,
+  // signed) | len << 16 | slot << 24, slot = span * kSlots + cut index.  A span's (at most
+  // kSlots) keys stay in its lane's registers until the sort (round 4; round 3: a list
+  // filled by LDS atomics inside the event walk, each append a wave-wide wait for its
+  // return).  (The block's LDS must stay within 17.5 KiB for 9 blocks per CU -- one
+  // 512-byte granule more gave 8 and cost pass A 11 %, round 4.)
+  __shared__ uint32_t s_sorted[kTThreads * kSlots];
   __shared__ uint32_t s_cls[8];        // keys per chunk-count class, then class offsets
   __shared__ typename hipcub::WarpReduce<LFn, 64>::TempStorage s_wred[kTThreads / 64];
-  __shared__ uint8_t s_ord[kListCap];  // list indices in class order
-  __shared__ uint8_t s_slot[kListCap];  // each listed key's span (in the block) * kSlots + cut index
   typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
   __shared__ typename NlScan::TempStorage tmp;
   uint8_t* blk = lds + PRE;  // block byte i at blk[16 + i]; the kPre bytes before the block below it
   const uint64_t bid = blockIdx.x;
-  if (threadIdx.x == 0) s_nk = 0;
   if (threadIdx.x < 8) s_cls[threadIdx.x] = 0;
   const uint64_t base = bid * kTChunk;
-  tsv_stage<PRE>(f, size, bid, lds);  // (its barrier publishes s_nk = 0)
+  tsv_stage<PRE>(f, size, bid, lds);  // (its barrier publishes s_cls = 0)
   const uint32_t rel = kTBytes * threadIdx.x;
   const uint8_t* span = blk + 16 + rel;
   const bool live = base + rel < size;
@@ -567,6 +565,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   uint32_t j = 0;                     // cut events so far
   int32_t lnl = -1;                   // the last newline's position in the block while no cut followed it
   uint32_t cut0 = 0xFFFFFFFFu;        // the span's first cut when no newline precedes it
+  constexpr uint32_t kNoKey = 0xFFFFFFFFu;
+  uint32_t key0 = kNoKey, key1 = kNoKey;  // the span's keys at cuts 0 and 1: start | len << 16
   if (live)
     span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
       acc = lfn_push<MDBM>(acc, t, rel + o + 1);
@@ -579,13 +579,11 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
         if (cut && j == 0 && lnl < 0 && !(nl & 1u)) cut0 = rel + o;
         const uint32_t len = rel + o - (uint32_t)(lnl + 1);
         if (cut && j < kSlots && lnl >= 0 && len <= kSpecLenMax) {
-          const uint32_t slot = atomicAdd(&s_nk, 1u);
-          if (slot < kListCap) {
-            s_key[slot] = ((uint32_t)(lnl + 1) & 0xFFFFu) | (len << 16);
-            s_slot[slot] = (uint8_t)(kSlots * threadIdx.x + j);
-            const uint32_t sh = j ? 56u : 48u;
-            pk = (pk & ~(0xFFull << sh)) | ((uint64_t)len << sh);
-          }
+          const uint32_t k = ((uint32_t)(lnl + 1) & 0xFFFFu) | (len << 16);
+          key0 = j ? key0 : k;
+          key1 = j ? k : key1;
+          const uint32_t sh = j ? 56u : 48u;
+          pk = (pk & ~(0xFFull << sh)) | ((uint64_t)len << sh);
         }
         lnl = cut ? -1 : t == 1u ? (int32_t)(rel + o) : lnl;
         j += cut ? 1u : 0u;
@@ -625,49 +623,42 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     }
     const uint32_t len = (uint32_t)((int32_t)cut0 - start);
     if (ok && len <= kSpecLenMax) {
-      const uint32_t slot = atomicAdd(&s_nk, 1u);
-      if (slot < kListCap) {
-        s_key[slot] = ((uint32_t)start & 0xFFFFu) | (len << 16);
-        s_slot[slot] = (uint8_t)(kSlots * threadIdx.x);
-        pk = (pk & ~(0xFFull << 48)) | ((uint64_t)len << 48);
-      }
+      key0 = ((uint32_t)start & 0xFFFFu) | (len << 16);
+      pk = (pk & ~(0xFFull << 48)) | ((uint64_t)len << 48);
     }
   }
   // a span with more than kEvCap events keeps its slots: pass B re-reads its events from
   // the file and counts its cuts the same way
   pk = over ? (kEvOverflow & ~kNoSlots) | (pk & kNoSlots) : pk | ((uint64_t)ne << 45);
   ev[base / kTBytes + threadIdx.x] = pk;
-  __syncthreads();
-  // The list's keys in order of chunk count (counting sort over 8 classes), so that each
-  // wave's hash loop runs as long as ITS longest key: on BASELINE-like files (keys 8-64 B,
-  // 1-4 chunks) wave 0 takes the short keys and runs 2 chunks instead of 4 (round 4).
-  const uint32_t nk = min(s_nk, kListCap);
-  static_assert(kListCap <= 2 * kTThreads, "two list keys per thread");
+  // The keys in order of chunk count (counting sort over 8 classes), so that each wave's
+  // hash loop runs as long as ITS longest key: on BASELINE-like files (keys 8-64 B, 1-4
+  // chunks) wave 0 takes the short keys and runs 2 chunks instead of 4 (round 4).
+  static_assert(kSlots == 2 && kSpecLenMax < 256 && kTThreads * kSlots <= 256, "slot | len | start in 32 bits");
   uint32_t cls[2];
+  const uint32_t kk[2] = {key0, key1};
 #pragma unroll
   for (uint32_t h = 0; h < 2; ++h) {
-    const uint32_t i = threadIdx.x + h * kTThreads;
-    cls[h] = i < nk ? min((s_key[i] >> 16) + 15u, 128u) / 16u : 0u;  // 0..8
+    cls[h] = min((kk[h] >> 16) + 15u, 128u) / 16u;  // 0..8
     cls[h] = cls[h] ? cls[h] - 1u : 0u;
-    if (i < nk) atomicAdd(&s_cls[cls[h]], 1u);
+    if (kk[h] != kNoKey) atomicAdd(&s_cls[cls[h]], 1u);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint32_t acc = 0;
+    uint32_t a = 0;
 #pragma unroll
     for (uint32_t c = 0; c < 8; ++c) {
       const uint32_t v = s_cls[c];
-      s_cls[c] = acc;
-      acc += v;
+      s_cls[c] = a;
+      a += v;
     }
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t h = 0; h < 2; ++h) {
-    const uint32_t i = threadIdx.x + h * kTThreads;
-    if (i < nk) s_ord[atomicAdd(&s_cls[cls[h]], 1u)] = (uint8_t)i;
-  }
+  for (uint32_t h = 0; h < 2; ++h)
+    if (kk[h] != kNoKey) s_sorted[atomicAdd(&s_cls[cls[h]], 1u)] = kk[h] | ((kSlots * threadIdx.x + h) << 24);
   __syncthreads();
+  const uint32_t nk = s_cls[7];  // (each class's offset has moved to its end: the last is the count)
   uint64_t raw[2];
   uint32_t slot[2];
 #pragma unroll
@@ -675,10 +666,9 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     const uint32_t q = threadIdx.x + h * kTThreads;
     slot[h] = 0xFFFFFFFFu;
     if (q < nk) {
-      const uint32_t i = s_ord[q];
-      const uint32_t k = s_key[i];
-      raw[h] = key_raw_lds(blk + 16 + (int16_t)(k & 0xFFFFu), k >> 16, sp);
-      slot[h] = s_slot[i];
+      const uint32_t k = s_sorted[q];
+      raw[h] = key_raw_lds(blk + 16 + (int16_t)(k & 0xFFFFu), (k >> 16) & 0xFFu, sp);
+      slot[h] = k >> 24;
     }
   }
   // The states go out as one 16-byte store per span (both slots; a slot no key took holds
