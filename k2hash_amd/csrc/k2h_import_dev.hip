@@ -556,7 +556,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   const bool live = base + rel < size;
   LFn acc = lfn_id();
   uint64_t pk = kNoSlots;
-  uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
+  uint32_t psh = 0, nl = 2u;  // psh: 9 x events so far; nl: no newline yet, and "no cut seen" (bit 1) until one is
   // Speculative keys, found in the same walk (round 4; round 3 walked the packed events a
   // second time after the block scan): a cut that follows a newline of this span ends the
   // key that starts after it; the span's first cut, if no newline precedes it here, waits
@@ -570,25 +570,29 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   if (live)
     span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
       acc = lfn_push<MDBM>(acc, t, rel + o + 1);
-      const uint64_t e = (uint64_t)(o | (t << 7)) << (9 * min(ne, kEvCap - 1));
-      pk |= (t && ne < kEvCap) ? e : 0ull;
-      ne += t ? 1u : 0u;
-      nl = t == 1u ? (1u | 2u | ((rel + o) << 2)) : t ? (nl & ~2u) : nl;
+      // (selects throughout: the branches hipcc made of these cost ~40 SALU per event)
+      const uint64_t e = (uint64_t)(o | (t << 7)) << (psh & 63u);
+      pk |= (t && psh < 9 * kEvCap) ? e : 0ull;
+      psh += t ? 9u : 0u;
+      const bool isnl = t == 1u;
+      const uint32_t nlv = 3u | ((rel + o) << 2), nlc = nl & (t ? ~2u : ~0u);
+      nl = isnl ? nlv : nlc;
       if constexpr (!MDBM) {
         const bool cut = t >= 2u;  // TAB or NUL
-        if (cut && j == 0 && lnl < 0 && !(nl & 1u)) cut0 = rel + o;
+        cut0 = (cut && j == 0 && lnl < 0 && !(nl & 1u)) ? rel + o : cut0;
         const uint32_t len = rel + o - (uint32_t)(lnl + 1);
-        if (cut && j < kSlots && lnl >= 0 && len <= kSpecLenMax) {
-          const uint32_t k = ((uint32_t)(lnl + 1) & 0xFFFFu) | (len << 16);
-          key0 = j ? key0 : k;
-          key1 = j ? k : key1;
-          const uint32_t sh = j ? 56u : 48u;
-          pk = (pk & ~(0xFFull << sh)) | ((uint64_t)len << sh);
-        }
-        lnl = cut ? -1 : t == 1u ? (int32_t)(rel + o) : lnl;
+        const bool em = cut && j < kSlots && lnl >= 0 && len <= kSpecLenMax;
+        const uint32_t k = ((uint32_t)(lnl + 1) & 0xFFFFu) | (len << 16);
+        key0 = (em && j == 0) ? k : key0;
+        key1 = (em && j != 0) ? k : key1;
+        const uint32_t sh = j ? 56u : 48u;
+        const uint64_t pkk = (pk & ~(0xFFull << sh)) | ((uint64_t)(len & 0xFFu) << sh);
+        pk = em ? pkk : pk;
+        lnl = cut ? -1 : isnl ? (int32_t)(rel + o) : lnl;
         j += cut ? 1u : 0u;
       }
     });
+  const uint32_t ne = psh / 9u;
   const bool over = ne > kEvCap;
   const LFn wf = wave_fn_reduce(s_wred[threadIdx.x >> 6], acc);
   if ((threadIdx.x & 63u) == 0) blk_fn[bid * kUnitsPerBlock + (threadIdx.x >> 6)] = gfn_of(wf, base);
