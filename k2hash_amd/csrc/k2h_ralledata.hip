@@ -187,7 +187,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
     in.soff = in.aoff = nullptr;
     in.skeys = in.attrs = nullptr;
   }
-  constexpr int R = kGatherRecs, NSEG = 5 * R;
+  // segments per record: header, key, value, subkeys, attributes (KV: the first three)
+  constexpr int NS = KV ? 3 : 5;
+  constexpr int R = kGatherRecs, NSEG = NS * R;
   typedef uint32_t u32x4_al __attribute__((ext_vector_type(4)));
   __shared__ __attribute__((aligned(16))) uint8_t img[kGatherImg];
   __shared__ uint32_t seg[NSEG + 1];  // segment g: seg_pack(adj, end): span byte y sits at img[y + adj], end in the span
@@ -295,14 +297,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
       *reinterpret_cast<u32x4_al*>(img + kGatherHdr + 80 * tid + 16 * c) = u32x4_al{f[4 * c], f[4 * c + 1], f[4 * c + 2], f[4 * c + 3]};
     int32_t start = B;
 #pragma unroll
-    for (int c = 0; c < 5; ++c) {
-      const uint32_t g = 5 * tid + c;
+    for (int c = 0; c < NS; ++c) {
+      const uint32_t g = NS * tid + c;
       const int32_t L = c == 0 ? 80 : (int32_t)len[c - 1];
       const int32_t adj = c == 0 ? kGatherHdr + 80 * (int32_t)tid - start : area[c - 1] + (int32_t)rel[c - 1] - start;
       seg[g] = seg_pack(adj, start + L);
       start += L;
     }
-    if (tid + 1 == nr) seg[5 * nr] = seg_pack(kGatherHdr, start);  // read (never used) as the last segment's successor
+    if (tid + 1 == nr) seg[NS * nr] = seg_pack(kGatherHdr, start);  // read (never used) as the last segment's successor
   }
 #pragma unroll
   for (int u = 0; u < PPT; ++u)
@@ -316,15 +318,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void r
   // later wait would include
   if (blob_off && tid >= 64 && tid - 64 < nr) {
     const uint32_t r = tid - 64;
-    blob_off[r0 + r] = o_first + (uint64_t)(uint32_t)(seg_unpack(seg[5 * r]).y - 80);
-    if (r0 + r + 1 == n) blob_off[n] = o_first + (uint64_t)(uint32_t)seg_unpack(seg[5 * nr]).y;
+    blob_off[r0 + r] = o_first + (uint64_t)(uint32_t)(seg_unpack(seg[NS * r]).y - 80);
+    if (r0 + r + 1 == n) blob_off[n] = o_first + (uint64_t)(uint32_t)seg_unpack(seg[NS * nr]).y;
   }
   // 1c'. the piece table, by waves 1-3 while wave 0 hashes (round 4: wave 0 built it in 1b,
   // one divergent loop trip per piece of each of its records' five segments -- ~200 M SALU
   // per call -- while the other waves waited at the barrier): each segment writes its index
   // for the pieces whose first byte it holds
   if (tid >= 64)
-    for (uint32_t g = tid - 64; g < 5 * nr; g += 192) {
+    for (uint32_t g = tid - 64; g < NS * nr; g += 192) {
       const int32_t end = seg_unpack(seg[g]).y, beg = g ? seg_unpack(seg[g - 1]).y : 0;
       for (int32_t p = g ? (beg + d0 + 15) >> 4 : 0; 16 * p - d0 < end; ++p) {
         tab[p] = (uint8_t)g;
