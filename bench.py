@@ -68,7 +68,7 @@ def parse(argv=None):
     p.add_argument("--warm-ms", type=float, default=150.0,
                    help="keep warming up (untimed) until at least this much GPU time has passed: the "
                         "MI355X clock ramps over the first ~30 ms of back-to-back launches "
-                        "(tools/clock_ramp.py, profiles/r01_clock_ramp.txt)")
+                        "(profiles/r01_clock_ramp.txt)")
     p.add_argument("--config", default=None, choices=sorted(CONFIGS),
                    help="default: fixed32 at N=1, fixed32_1g (config 4) at N>1")
     p.add_argument("--second", action="store_true", help="also emit the second hash (h2)")
@@ -511,21 +511,15 @@ def valu_fields(name: str, kern_s: float, model_insts: float, keys: int | None =
     """VALU-issue roofline: wave64 VALU instructions per launch (rocprofv3 SQ_INSTS_VALU pass,
     profiles/valu_<name>.json scaled to this launch's key count, else the FNV-step model) at
     the peak issue rate, over the measured launch time."""
-    insts, src, clock = model_insts, "model: 86 slow-issue VALU ops per 16-byte chunk per 64 keys", None
+    insts, src = model_insts, "model: 86 slow-issue VALU ops per 16-byte chunk per 64 keys"
     d, scale = _profile("valu", name, keys)
     if d is not None:
         insts = float(d["valu_insts_per_launch"]) * scale
         src = (f"profiles/valu_{name}.json ({d.get('round', '')}; {d['keys_per_launch']} keys per profiled launch, "
                f"scaled x{scale:.4g} to this launch)")
-    probe = ROOT / "profiles" / "clock_probe.json"  # tools/clock_probe.py: s_memtime / s_memrealtime per wave
-    if probe.exists():
-        clock = json.loads(probe.read_text()).get(name, {}).get("clock_ghz")
     floor_s = insts * VALU_CYCLES_PER_INST / (VALU_SIMDS * VALU_PEAK_HZ)
     r = {"valu_frac": floor_s / kern_s, "valu_insts_per_launch": insts, "valu_floor_us": floor_s * 1e6,
          "valu_source": src}
-    if clock:  # the same floor at the shader clock the waves ran at under this kernel (power-limited)
-        r["valu_frac_at_measured_clock"] = floor_s * VALU_PEAK_HZ / (clock * 1e9) / kern_s
-        r["measured_clock_ghz"] = clock
     return r
 
 

@@ -868,8 +868,10 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       if (hit) {
         a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
         c = e > s.fs ? raw : a;
-      } else {
+      } else if (s.fs <= e && e <= size) {
         hash_cstr(f, s.fs, e - s.fs, sp, a, c);
+      } else {  // a state outside the file (never for correct states): wrong records, not a fault
+        a = c = 0;
       }
       if (staged) {
         s_h[2 * x] = a;

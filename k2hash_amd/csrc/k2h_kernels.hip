@@ -181,7 +181,7 @@ hipError_t launch_bucket_index(const uint64_t* h1, uint64_t n, const BucketParam
 // Default kernel per shape (the product path).  32-byte keys at a 16-aligned base: one-wave
 // blocks, two keys per lane with all four loads issued before the first hash (a wave keeps
 // 4 KiB in flight and half as many waves need dispatching; round-1 A/B).
-// Other lengths (tools/fixed_sweep.py): up to 32 B the per-lane tail loop, below 128 B
+// Other lengths: up to 32 B the per-lane tail loop, below 128 B
 // per-lane direct 16-byte loads, from 128 B on the line-DMA kernel (multiples of 128 B at a
 // 128-aligned base) or the cooperative line ring.
 hipError_t launch_fixed(const void* keys, uint64_t key_len, uint64_t n, uint64_t seed, uint64_t* h1, uint64_t* h2,

@@ -119,3 +119,17 @@ def test_import_kernels_use_no_scratch_and_keep_pass_a_occupancy(import_asm):
     assert len(pass_a) == 1
     assert pass_a[0]["group_segment_fixed_size"] <= 35 * 512
     assert pass_a[0]["vgpr_count"] <= 64  # 8 waves per SIMD's worth of registers; LDS sets 4.5
+
+
+def test_import_file_reads_are_bounds_guarded():
+    """Every device hash of a key read from the file (hash_cstr) is guarded by a range check
+    against the file size (ADVICE r4: pass B's miss path faulted on a probe's wrong states;
+    a wrong state must give wrong records that parity catches, not a device fault)."""
+    text = (CSRC / "k2h_import_dev.hip").read_text()
+    calls = [m.start() for m in re.finditer(r"\bhash_cstr\(f,", text)]
+    assert len(calls) >= 2
+    for pos in calls:
+        line = text[text.rfind("\n", 0, pos) + 1:text.find("\n", pos)]
+        prev = text[text.rfind("\n", 0, text.rfind("\n", 0, pos)) + 1:pos]
+        guarded = ("<= size" in line) or ("<= size" in prev)
+        assert guarded, line.strip()

@@ -5,3 +5,4 @@
 #include "lab_lines.inc"
 #include "lab_csr_setup.inc"
 #include "lab_csr.inc"
+#include "lab_csr_rs.inc"

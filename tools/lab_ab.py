@@ -35,6 +35,11 @@ def lab_lib():
     if hasattr(lib, "k2h_lab_csr"):
         lib.k2h_lab_csr.restype = ctypes.c_int
         lib.k2h_lab_csr.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+    if hasattr(lib, "k2h_lab_csr_rs"):
+        lib.k2h_lab_csr_rs.restype = ctypes.c_int
+        lib.k2h_lab_csr_rs.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+        lib.k2h_lab_simd_probe.restype = ctypes.c_int
+        lib.k2h_lab_simd_probe.argtypes = [_p, ctypes.c_uint, _p]
     if hasattr(lib, "k2h_lab_ralle"):
         lib.k2h_lab_ralle.restype = ctypes.c_int
         lib.k2h_lab_ralle.argtypes = [ctypes.c_int, _p, _p, _p, _p, _u64, _p, _p, _p]
@@ -48,6 +53,8 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--launches", type=int, default=20)
     ap.add_argument("--warm-ms", type=float, default=200.0)
+    ap.add_argument("--simd-probe", action="store_true")
+    ap.add_argument("--rs-stats", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -103,9 +110,32 @@ def main():
         chunks = gold["csr_8_256_64M"]["chunks"]
 
         def launch(v):
-            rc = lib.k2h_lab_csr(int(v), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
-                                 ctypes.c_void_p(h1.data_ptr()), None, sh)
+            fn = lib.k2h_lab_csr_rs if int(v) >= 20 else lib.k2h_lab_csr  # 20-22: lab_csr_rs.inc
+            rc = fn(int(v), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
+                    ctypes.c_void_p(h1.data_ptr()), None, sh)
             assert rc == 0, rc
+
+        if args.simd_probe:  # SIMD (HW_ID bits 5:4) of each wave of the first 4 blocks of 512 threads
+            out = torch.zeros(64, dtype=torch.int32, device=dev)
+            assert lib.k2h_lab_simd_probe(ctypes.c_void_p(out.data_ptr()), 4, sh) == 0
+            torch.cuda.synchronize()
+            hw = [int(x) & 0xFFFFFFFF for x in out[:32].cpu()]
+            print(json.dumps({"hw_id": [hex(h) for h in hw],
+                              "simd_of_wave": [[(h >> 4) & 3 for h in hw[8 * b:8 * b + 8]] for b in range(4)]}))
+        if args.rs_stats:  # variant 23: the role-split kernel with per-hash-wave phase clocks
+            st = torch.zeros(256 * 4 * 8, dtype=torch.int64, device=dev)
+            for _ in range(3):
+                rc = lib.k2h_lab_csr_rs(23, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
+                                        ctypes.c_void_p(h1.data_ptr()), ctypes.c_void_p(st.data_ptr()), sh)
+                assert rc == 0, rc
+            torch.cuda.synchronize()
+            a = st.view(-1, 8)[:, :5].cpu().double()
+            us = a[:, :4].mean(0) * 0.01  # memrealtime ticks (100 MHz) -> us
+            steps = a[:, 4].mean().item()
+            print(json.dumps({"rs_stats_us_per_hash_wave": {"prologue": us[0].item(), "walk": us[1].item(),
+                              "epilogue": us[2].item(), "barrier": us[3].item()},
+                              "steps_per_hash_wave": steps, "walk_ns_per_step": us[1].item() * 1e3 / steps,
+                              "verify": bench.verify_chunks(h1, 0, chunks)}))
 
     res = {}
     for v in args.variants:  # parity first
