@@ -139,20 +139,40 @@ def _fuzz_file(rng, size, fmt):
     return body
 
 
+def _check_fused(f, data, fmt, host, what):
+    """import_scan_prehash_device on the device file `f` == the host scan + the host prehash."""
+    import torch
+    recs, h1, h2 = archive.import_scan_prehash_device(f, fmt)
+    torch.cuda.synchronize()
+    a = recs.cpu().numpy().view(np.uint64)
+    assert a.shape[0] == host.size, what
+    for i, name in enumerate(archive.IMPORT_DTYPE.names):
+        assert np.array_equal(a[:, i], host[name]), (what, name)
+    if host.size:
+        e1, e2 = archive.import_prehash(data, host)
+        assert np.array_equal(h1.cpu().numpy().view(np.uint64), e1), what
+        assert np.array_equal(h2.cpu().numpy().view(np.uint64), e2), what
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("fmt", ["tsv", "mdbm"])
 def test_device_scan_fuzz(cuda, fmt):
     """Random files over a small alphabet (keys across newlines, values with TABs and
     NULs, every EOF shape), sizes across the 64-byte thread span and 16 KiB block
-    boundaries, and unaligned device bases: device scan == host scan."""
+    boundaries, and unaligned device bases: device scan == host scan, and the fused scan +
+    prehash (pass A's speculative head keys, slots matched by length, more than five events
+    per span) == host scan + host prehash."""
     rng = np.random.default_rng(0x6B32 + (fmt == "mdbm"))
     # (8 MiB + 40001: two tiles of the TSV entry-state scan, the second one partial)
     sizes = list(range(0, 80)) + [127, 128, 129, 16383, 16384, 16385, 40000, 200001, (8 << 20) + 40001]
     for k, size in enumerate(sizes):
         data = _fuzz_file(rng, size, fmt)
         shift = k % 5
-        _, _, got = _dev_scan_np(cuda, data, fmt, shift)
-        assert np.array_equal(got, archive.import_scan(data, fmt)), (fmt, size, shift)
+        f, _, got = _dev_scan_np(cuda, data, fmt, shift)
+        host = archive.import_scan(data, fmt)
+        assert np.array_equal(got, host), (fmt, size, shift)
+        if size <= 200001 or k == len(sizes) - 1:  # the fused scan + prehash (speculative head keys) too
+            _check_fused(f, data, fmt, host, (fmt, size, shift))
     # EOF shapes of the mdbm header itself
     if fmt == "mdbm":
         hdr = b"a\nb\nc\nd\nHEADER=END"
@@ -393,3 +413,32 @@ def test_fused_scan_prehash_staged_and_direct_units(cuda):
     e1, e2 = archive.import_prehash(data, host)
     assert np.array_equal(h1.cpu().numpy().view(np.uint64), e1)
     assert np.array_equal(h2.cpu().numpy().view(np.uint64), e2)
+
+
+@pytest.mark.gpu
+def test_fused_scan_prehash_mdbm_staged_and_direct_units(cuda):
+    """mdbm through the shared scan: a multi-MB body of key and value lines in
+    runs of record sizes on both sides of pass B's 96-record staging limit, records
+    straddling unit boundaries, keys with NULs, and a key line at EOF (one more record whose
+    value is the previous record's, fixed up by the host after the call): the fused call's
+    records and hashes equal the host scan and the host prehash."""
+    import torch
+    rng = np.random.default_rng(0x3D8B)
+    parts = [b"format=print\ntype=btree\nmdbm_pagesize=4096\nmdbm_pagecount=1\nHEADER=END\n"]
+    nrec = 0
+    for n, klo, khi, vlo, vhi in ((20000, 1, 9, 0, 12), (12000, 8, 40, 55, 63), (8000, 8, 64, 60, 180),
+                                  (20000, 1, 9, 0, 12), (12000, 8, 40, 55, 63)):
+        for _ in range(n):
+            k = bytes(rng.integers(33, 127, int(rng.integers(klo, khi + 1)), dtype=np.uint8))
+            v = bytes(rng.integers(9, 127, int(rng.integers(vlo, vhi + 1)), dtype=np.uint8)).replace(b"\n", b"x")
+            if rng.random() < 0.01:
+                k = k[:1] + b"\x00" + k[1:]
+            parts.append(k + b"\n" + v + b"\n")
+            nrec += 1
+    parts.append(b"tail-key-at-eof")
+    data = b"".join(parts)
+    assert len(data) > 2 << 20
+    f = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda)
+    host = archive.import_scan(data, "mdbm")
+    assert host.size == nrec + 1
+    _check_fused(f, data, "mdbm", host, "mdbm")

@@ -6,3 +6,4 @@
 #include "lab_csr_setup.inc"
 #include "lab_csr.inc"
 #include "lab_csr_rs.inc"
+#include "lab_csr_rs2.inc"

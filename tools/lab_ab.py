@@ -38,6 +38,8 @@ def lab_lib():
     if hasattr(lib, "k2h_lab_csr_rs"):
         lib.k2h_lab_csr_rs.restype = ctypes.c_int
         lib.k2h_lab_csr_rs.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+        lib.k2h_lab_csr_rs2.restype = ctypes.c_int
+        lib.k2h_lab_csr_rs2.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
         lib.k2h_lab_simd_probe.restype = ctypes.c_int
         lib.k2h_lab_simd_probe.argtypes = [_p, ctypes.c_uint, _p]
     if hasattr(lib, "k2h_lab_ralle"):
@@ -55,6 +57,7 @@ def main():
     ap.add_argument("--warm-ms", type=float, default=200.0)
     ap.add_argument("--simd-probe", action="store_true")
     ap.add_argument("--rs-stats", action="store_true")
+    ap.add_argument("--rs-steps", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -110,7 +113,8 @@ def main():
         chunks = gold["csr_8_256_64M"]["chunks"]
 
         def launch(v):
-            fn = lib.k2h_lab_csr_rs if int(v) >= 20 else lib.k2h_lab_csr  # 20-22: lab_csr_rs.inc
+            # 20-25: lab_csr_rs.inc, 30-32: lab_csr_rs2.inc
+            fn = lib.k2h_lab_csr_rs2 if int(v) >= 30 else lib.k2h_lab_csr_rs if int(v) >= 20 else lib.k2h_lab_csr
             rc = fn(int(v), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
                     ctypes.c_void_p(h1.data_ptr()), None, sh)
             assert rc == 0, rc
@@ -122,6 +126,16 @@ def main():
             hw = [int(x) & 0xFFFFFFFF for x in out[:32].cpu()]
             print(json.dumps({"hw_id": [hex(h) for h in hw],
                               "simd_of_wave": [[(h >> 4) & 3 for h in hw[8 * b:8 * b + 8]] for b in range(4)]}))
+        if args.rs_steps:  # executed walk steps per hash wave and tile (pairs of sorted ranks i, 511-i)
+            import numpy as np
+            o = off.cpu().numpy()
+            k = (np.diff(o) + 15) // 16
+            nt = n // 512
+            k = np.sort(np.minimum(k[:nt * 512], 63).reshape(nt, 512), axis=1)
+            A, B = k[:, :256].reshape(nt, 4, 64), k[:, ::-1][:, :256].reshape(nt, 4, 64)
+            print(json.dumps({"rs_steps_per_wave_tile": {
+                "pair_max": float((A + B).max(-1).mean()), "phase_max": float((A.max(-1) + B.max(-1)).mean()),
+                "ideal": float((A + B).mean()), "tiles_per_cu": nt / 256}}))
         if args.rs_stats:  # variant 23: the role-split kernel with per-hash-wave phase clocks
             st = torch.zeros(256 * 4 * 8, dtype=torch.int64, device=dev)
             for _ in range(3):
