@@ -7,3 +7,5 @@
 #include "lab_csr.inc"
 #include "lab_csr_rs.inc"
 #include "lab_csr_rs2.inc"
+#include "lab_csr_rs4.inc"
+#include "lab_csr_lean.inc"

@@ -40,6 +40,10 @@ def lab_lib():
         lib.k2h_lab_csr_rs.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
         lib.k2h_lab_csr_rs2.restype = ctypes.c_int
         lib.k2h_lab_csr_rs2.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+        lib.k2h_lab_csr_rs4.restype = ctypes.c_int
+        lib.k2h_lab_csr_rs4.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+        lib.k2h_lab_csr_lean.restype = ctypes.c_int
+        lib.k2h_lab_csr_lean.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
         lib.k2h_lab_simd_probe.restype = ctypes.c_int
         lib.k2h_lab_simd_probe.argtypes = [_p, ctypes.c_uint, _p]
     if hasattr(lib, "k2h_lab_ralle"):
@@ -58,6 +62,7 @@ def main():
     ap.add_argument("--simd-probe", action="store_true")
     ap.add_argument("--rs-stats", action="store_true")
     ap.add_argument("--rs-steps", action="store_true")
+    ap.add_argument("--rs2-stats", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -113,8 +118,9 @@ def main():
         chunks = gold["csr_8_256_64M"]["chunks"]
 
         def launch(v):
-            # 20-25: lab_csr_rs.inc, 30-32: lab_csr_rs2.inc
-            fn = lib.k2h_lab_csr_rs2 if int(v) >= 30 else lib.k2h_lab_csr_rs if int(v) >= 20 else lib.k2h_lab_csr
+            # 20-27: lab_csr_rs.inc, 30-33: lab_csr_rs2.inc, 40-42: lab_csr_rs4.inc, 50-52: lab_csr_lean.inc
+            fn = (lib.k2h_lab_csr_lean if int(v) >= 50 else lib.k2h_lab_csr_rs4 if int(v) >= 40 else lib.k2h_lab_csr_rs2 if int(v) >= 30 else
+                  lib.k2h_lab_csr_rs if int(v) >= 20 else lib.k2h_lab_csr)
             rc = fn(int(v), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
                     ctypes.c_void_p(h1.data_ptr()), None, sh)
             assert rc == 0, rc
@@ -136,6 +142,19 @@ def main():
             print(json.dumps({"rs_steps_per_wave_tile": {
                 "pair_max": float((A + B).max(-1).mean()), "phase_max": float((A.max(-1) + B.max(-1)).mean()),
                 "ideal": float((A + B).mean()), "tiles_per_cu": nt / 256}}))
+        if args.rs2_stats:  # variant 33: rs2 with per-hash-wave phase clocks (8 hash waves)
+            st = torch.zeros(256 * 8 * 8, dtype=torch.int64, device=dev)
+            for _ in range(3):
+                rc = lib.k2h_lab_csr_rs2(33, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
+                                         ctypes.c_void_p(h1.data_ptr()), ctypes.c_void_p(st.data_ptr()), sh)
+                assert rc == 0, rc
+            torch.cuda.synchronize()
+            a = st.view(256, 8, 8)[:, :, :5].cpu().double()
+            us = a[:, :, :4].mean(0) * 0.01  # per hash wave index, ticks (100 MHz) -> us
+            print(json.dumps({"rs2_stats_us_by_wave": {"ready_wait": us[:, 0].tolist(), "prologue": us[:, 1].tolist(),
+                              "walk": us[:, 2].tolist(), "epilogue_done": us[:, 3].tolist()},
+                              "steps_by_wave": a[:, :, 4].mean(0).tolist(),
+                              "verify": bench.verify_chunks(h1, 0, chunks)}))
         if args.rs_stats:  # variant 23: the role-split kernel with per-hash-wave phase clocks
             st = torch.zeros(256 * 4 * 8, dtype=torch.int64, device=dev)
             for _ in range(3):

@@ -31,7 +31,7 @@ def main():
         out = torch.zeros(n, dtype=torch.int64, device=dev)
         assert lib.k2h_lab_csr(0, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
                                ctypes.c_void_p(ref.data_ptr()), None, sh) == 0
-        fn = lib.k2h_lab_csr_rs2 if v >= 30 else lib.k2h_lab_csr_rs
+        fn = lib.k2h_lab_csr_rs4 if v >= 40 else lib.k2h_lab_csr_rs2 if v >= 30 else lib.k2h_lab_csr_rs
         assert fn(v, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
                   ctypes.c_void_p(out.data_ptr()), None, sh) == 0
         torch.cuda.synchronize()
