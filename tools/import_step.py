@@ -4,6 +4,9 @@
 
     rocprofv3 ... -- python3 tools/import_step.py [--calls K]
 
+With --mdbm: the same records in mdbm's print format (built on the device, records checked
+against the generator and hashes against the ranges path), timed per call.
+
 With --ab LIB: same-process A/B of the working tree's library against another build of it
 (tools/build_ab.sh), interleaved rounds, each library's result checked against
 tests/golden/import_digest.json first.
@@ -33,9 +36,45 @@ def _verify(out):
     return g["records"] == recs.shape[0] and all(bench.digest_dev(v.contiguous(), 0) == g[k] for k, v in cols.items())
 
 
+MDBM_HDR = b"format=print\ntype=btree\nmdbm_pagesize=4096\nmdbm_pagecount=1\nHEADER=END\n"
+
+
+def mdbm_workload(dev):
+    """The same 2^23 records as bench.import_workload in mdbm's print format (a key line and
+    a value line per record after the five header lines, tests/k2himport.cc:95-117), built
+    on the device; returns the file and each record's expected (key_off, key_len, val_off,
+    val_len)."""
+    from k2hash_amd import batch
+    n = bench.IMPORT_N
+    kl = batch.synth_offsets(n, dev, *bench.IMPORT_KEY_LENS, seed=batch.SEED_LENS + 11).diff()
+    vl = batch.synth_offsets(n, dev, *bench.IMPORT_VAL_LENS, seed=batch.SEED_LENS + 13).diff()
+    h = len(MDBM_HDR)
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(kl + vl + 2, dim=0, out=off[1:])
+    off += h
+    data = batch.synth_bytes(int(off[-1].item()), dev, byte_off=bench.IMPORT_BYTE_OFF)
+    data.remainder_(95).add_(32)
+    data[:h] = torch.frombuffer(bytearray(MDBM_HDR), dtype=torch.uint8).to(dev)
+    data[off[:-1] + kl] = 10
+    data[off[1:] - 1] = 10
+    exp = torch.stack([off[:-1], kl, off[:-1] + kl + 1, vl], dim=1)
+    return data, exp
+
+
+def verify_mdbm(out, data, exp):
+    """Records equal the generator's; h1 / h2 equal the ranges path's C-string hashes of the
+    same keys (k2h_amd_hash_ranges, CSTR: another product kernel, not the oracle)."""
+    recs, h1, h2 = out
+    if recs.shape != exp.shape or not torch.equal(recs, exp):
+        return False
+    g1, g2 = archive.hash_ranges(data, exp[:, 0].contiguous(), exp[:, 1].contiguous(), second=True, cstr=True)
+    return bool(torch.equal(g1, h1) and torch.equal(g2, h2))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--calls", type=int, default=10)
+    ap.add_argument("--mdbm", action="store_true", help="time the mdbm scan (the same records in mdbm's print format)")
     ap.add_argument("--ab", default="", help="another build of libk2hash_amd.so to time against the tree's")
     ap.add_argument("--rounds", type=int, default=9)
     ap.add_argument("--lib", default="", help="run (and profile) this build instead of the tree's")
@@ -43,6 +82,25 @@ def main():
                     "the digest check (their results may be wrong by design)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if a.mdbm:  # one verified call, then the timed calls
+        data, exp = mdbm_workload(dev)
+        ok = verify_mdbm(archive.import_scan_prehash_device(data, "mdbm"), data, exp)
+        print(json.dumps({"mdbm_bytes": data.numel(), "records": int(exp.shape[0]), "verify_ok": ok}), flush=True)
+        if not ok:
+            sys.exit(1)
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < 0.15:
+            archive.import_scan_prehash_device(data, "mdbm")
+        torch.cuda.synchronize()
+        ts = []
+        for _ in range(a.rounds):
+            t0 = time.perf_counter()
+            for _ in range(a.calls):
+                archive.import_scan_prehash_device(data, "mdbm")
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - t0) / a.calls * 1e3)
+        print(json.dumps({"mdbm_ms_per_call_median": statistics.median(ts), "min": min(ts), "all": ts}))
+        return
     data = bench.import_workload(dev)
     if a.lib:
         _native._batch = _native._bind(ctypes.CDLL(str(Path(a.lib).resolve())), _native.SIGNATURES.keys())

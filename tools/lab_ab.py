@@ -44,6 +44,8 @@ def lab_lib():
         lib.k2h_lab_csr_rs4.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
         lib.k2h_lab_csr_lean.restype = ctypes.c_int
         lib.k2h_lab_csr_lean.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+        lib.k2h_lab_csr_lean4.restype = ctypes.c_int
+        lib.k2h_lab_csr_lean4.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
         lib.k2h_lab_simd_probe.restype = ctypes.c_int
         lib.k2h_lab_simd_probe.argtypes = [_p, ctypes.c_uint, _p]
     if hasattr(lib, "k2h_lab_ralle"):
@@ -118,8 +120,8 @@ def main():
         chunks = gold["csr_8_256_64M"]["chunks"]
 
         def launch(v):
-            # 20-27: lab_csr_rs.inc, 30-33: lab_csr_rs2.inc, 40-42: lab_csr_rs4.inc, 50-52: lab_csr_lean.inc
-            fn = (lib.k2h_lab_csr_lean if int(v) >= 50 else lib.k2h_lab_csr_rs4 if int(v) >= 40 else lib.k2h_lab_csr_rs2 if int(v) >= 30 else
+            # 20-27: lab_csr_rs.inc, 30-33: lab_csr_rs2.inc, 40-42: lab_csr_rs4.inc, 50-54: lab_csr_lean.inc
+            fn = (lib.k2h_lab_csr_lean4 if int(v) >= 53 else lib.k2h_lab_csr_lean if int(v) >= 50 else lib.k2h_lab_csr_rs4 if int(v) >= 40 else lib.k2h_lab_csr_rs2 if int(v) >= 30 else
                   lib.k2h_lab_csr_rs if int(v) >= 20 else lib.k2h_lab_csr)
             rc = fn(int(v), ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
                     ctypes.c_void_p(h1.data_ptr()), None, sh)
