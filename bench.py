@@ -915,9 +915,22 @@ def main():
     if strong:
         total = args.keys or (KEYS_1G if n is None else n)
         if kind == "csr":
-            off_g = batch.synth_offsets(total, dev, shape[0], shape[1])  # the whole batch's offsets
-            cuts = shard.csr_cuts(off_g, world)
-            cut_bytes = [int(off_g[b].item()) - int(off_g[a].item()) for a, b in cuts]
+            # The byte cuts once, on rank 0 (the whole batch's offsets: 2^26 + 1 int64), then
+            # broadcast as the world + 1 key cuts and their byte offsets; every rank then
+            # synthesises only its own keys' offsets (a key's length is a function of its
+            # index), rebased to its first byte (each rank built the whole array).
+            plan = torch.zeros(2 * (world + 1), dtype=torch.int64,
+                               device=dev if args.backend == "nccl" else "cpu")
+            if rank == 0:
+                off_g = batch.synth_offsets(total, dev, shape[0], shape[1])
+                ks = [a for a, _ in shard.csr_cuts(off_g, world)] + [total]
+                plan.copy_(torch.tensor(ks + [int(off_g[k].item()) for k in ks], dtype=torch.int64))
+                del off_g
+            if world > 1:
+                dist.broadcast(plan, 0)
+            ks, bs = plan[:world + 1].tolist(), plan[world + 1:].tolist()
+            cuts = [(ks[r], ks[r + 1]) for r in range(world)]
+            cut_bytes = [bs[r + 1] - bs[r] for r in range(world)]
             first, last = cuts[rank]
         else:
             first, last = shard.shard_range(total, rank, world)
@@ -947,9 +960,8 @@ def main():
             algo_bytes = max(algo_bytes, (kb + vb + 16 * (n + 1)) + (80 * n + kb + vb + 8 * (n + 1)))
             key_bytes = max(key_bytes, kb)
         elif strong:  # this rank's byte range of the one reference batch (byte stream offset = its first byte)
-            off = shard.rebase_offsets(off_g, first, last).contiguous()
-            b0 = int(off_g[first].item())
-            del off_g
+            off = batch.synth_offsets(last - first, dev, shape[0], shape[1], first_key=first)
+            b0 = bs[rank]
             nb = int(off[-1].item())
             data = batch.synth_bytes(nb, dev, byte_off=b0)
             sets.append((data, off))
