@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Table of PMC counters per variant from a tools/pmc_variants.sh output directory:
+"""Table of PMC counters per variant from an output directory of the round-2 tools/pmc_variants.sh (at commit f74668a):
 per-dispatch sums over XCDs, median over dispatches of the hash kernel, plus the derived
 clock (GRBM_GUI_ACTIVE per XCD / duration) and VALU issue utilisation
 (SQ_INSTS_VALU x 4.19 cycles / (SIMDs x cycles)).   usage: pmc_table.py <dir> [kernel-substring]"""

@@ -56,10 +56,12 @@ def main():
     (prof / "traffic_import.json").write_text(json.dumps({
         "kernel": kern, "hbm_bytes_per_launch": traffic, "FETCH_SIZE_kB": pmc["FETCH_SIZE"],
         "WRITE_SIZE_kB": pmc["WRITE_SIZE"], "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
-        "round": tag, "keys_per_launch": 1 << 23}, indent=1) + "\n")
+        "round": tag, "keys_per_launch": 1 << 23,
+        "written_by": "tools/summarize_import_profile.py over tools/gpu/import_prof.sh"}, indent=1) + "\n")
     (prof / "valu_import.json").write_text(json.dumps({
         "kernel": kern, "valu_insts_per_launch": pmc["SQ_INSTS_VALU"], "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"),
-        "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"), "round": tag, "keys_per_launch": 1 << 23}, indent=1) + "\n")
+        "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"), "round": tag, "keys_per_launch": 1 << 23,
+        "written_by": "tools/summarize_import_profile.py over tools/gpu/import_prof.sh"}, indent=1) + "\n")
     s = {"per_kernel_us_per_call": {k: v / 1e3 for k, v in per.items()}, "gpu_us_per_call": gpu_us,
          "pmc_per_call": pmc, "hbm_bytes_per_call": traffic,
          "source": "tools/gpu/import_prof.sh: rocprofv3 over tools/import_step.py (8M-record TSV, 1.16 GB)"}

@@ -64,6 +64,7 @@ for d in sorted(p for p in src.iterdir() if p.is_dir() and "_pmc" not in p.name)
             "kernel": top["Name"], "hbm_bytes_per_launch": traffic, "FETCH_SIZE_kB": pmc["FETCH_SIZE"],
             "WRITE_SIZE_kB": pmc["WRITE_SIZE"], "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
             "source": f"profiles/{tag}_{cfg}_summary.json (rocprofv3 --pmc passes)", "round": tag,
+            "written_by": "tools/summarize_profiles.py over tools/profile_round.sh (tools/gpu/final.sh)",
             "keys_per_launch": keys}, indent=1))
     if "SQ_INSTS_VALU" in pmc:
         (dst / f"valu_{cfg}.json").write_text(json.dumps({
@@ -71,6 +72,7 @@ for d in sorted(p for p in src.iterdir() if p.is_dir() and "_pmc" not in p.name)
             "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"), "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"),
             "waves_per_launch": pmc.get("SQ_WAVES"),
             "source": f"profiles/{tag}_{cfg}_summary.json (rocprofv3 --pmc SQ_INSTS_VALU pass)", "round": tag,
+            "written_by": "tools/summarize_profiles.py over tools/profile_round.sh (tools/gpu/final.sh)",
             "keys_per_launch": keys}, indent=1))
     s = {"window": window, "pmc_per_launch": pmc, "hbm_bytes_per_launch": traffic}
     if line:
