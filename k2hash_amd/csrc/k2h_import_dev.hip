@@ -561,10 +561,14 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   // second time after the block scan): a cut that follows a newline of this span ends the
   // key that starts after it; the span's first cut, if no newline precedes it here, waits
   // for the scan (cut0) -- the entering state decides whether it ends a key, and where
-  // that key starts.
+  // that key starts.  The walk only records the span's first two cuts with the newline
+  // state they met; the keys are assembled after it (round 5: a wave walks as many events
+  // as its busiest lane, so per-event instructions cost 2.5x their mean share).
   uint32_t j = 0;                     // cut events so far
   int32_t lnl = -1;                   // the last newline's position in the block while no cut followed it
-  uint32_t cut0 = 0xFFFFFFFFu;        // the span's first cut when no newline precedes it
+  uint32_t cp[kSlots] = {0, 0};       // cut h's position, h < kSlots
+  int32_t cl[kSlots] = {-1, -1};      // ... and lnl when it was read
+  uint32_t ns0 = 0;                   // a newline preceded cut 0 in the span
   constexpr uint32_t kNoKey = 0xFFFFFFFFu;
   uint32_t key0 = kNoKey, key1 = kNoKey;  // the span's keys at cuts 0 and 1: start | len << 16
   if (live)
@@ -579,19 +583,30 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
       nl = isnl ? nlv : nlc;
       if constexpr (!MDBM) {
         const bool cut = t >= 2u;  // TAB or NUL
-        cut0 = (cut && j == 0 && lnl < 0 && !(nl & 1u)) ? rel + o : cut0;
-        const uint32_t len = rel + o - (uint32_t)(lnl + 1);
-        const bool em = cut && j < kSlots && lnl >= 0 && len <= kSpecLenMax;
-        const uint32_t k = ((uint32_t)(lnl + 1) & 0xFFFFu) | (len << 16);
-        key0 = (em && j == 0) ? k : key0;
-        key1 = (em && j != 0) ? k : key1;
-        const uint32_t sh = j ? 56u : 48u;
-        const uint64_t pkk = (pk & ~(0xFFull << sh)) | ((uint64_t)(len & 0xFFu) << sh);
-        pk = em ? pkk : pk;
+        const bool c0 = cut && j == 0, c1 = cut && j == 1;
+        cp[0] = c0 ? rel + o : cp[0];
+        cl[0] = c0 ? lnl : cl[0];
+        ns0 = c0 ? nl & 1u : ns0;
+        cp[1] = c1 ? rel + o : cp[1];
+        cl[1] = c1 ? lnl : cl[1];
         lnl = cut ? -1 : isnl ? (int32_t)(rel + o) : lnl;
         j += cut ? 1u : 0u;
       }
     });
+  uint32_t cut0 = 0xFFFFFFFFu;  // the span's first cut when no newline precedes it
+  if constexpr (!MDBM) {
+#pragma unroll
+    for (uint32_t h = 0; h < kSlots; ++h) {
+      const uint32_t len = cp[h] - (uint32_t)(cl[h] + 1);
+      const bool em = j > h && cl[h] >= 0 && len <= kSpecLenMax;
+      const uint32_t k = ((uint32_t)(cl[h] + 1) & 0xFFFFu) | (len << 16);
+      if (h == 0) key0 = em ? k : kNoKey;
+      else key1 = em ? k : kNoKey;
+      const uint64_t pkk = (pk & ~(0xFFull << (48 + 8 * h))) | ((uint64_t)(len & 0xFFu) << (48 + 8 * h));
+      pk = em ? pkk : pk;
+    }
+    cut0 = (j > 0 && cl[0] < 0 && !ns0) ? cp[0] : cut0;
+  }
   const uint32_t ne = psh / 9u;
   const bool over = ne > kEvCap;
   const LFn wf = wave_fn_reduce(s_wred[threadIdx.x >> 6], acc);
