@@ -373,6 +373,56 @@ __device__ inline LFn lfn_push(const LFn& a, uint32_t t, uint32_t p1) {
              (a.last & ~take) | ((p1 | (p1 << 16)) & take), t == 3u ? p1 : a.c};
 }
 
+// The function of a span's packed events (at most kEvCap, pass A's word) by table (round 5):
+// it depends on their types and offsets only, so a 1024-entry table indexed by the five
+// 2-bit types (0: none) gives, per entry mode, the exit mode, the record ends and the index
+// of the last field boundary, plus the index of the last NUL; the offsets come from the
+// word.  Pass B built it with one lfn_push per event, and a wave ran as many as its busiest
+// lane (4.7 per span against a mean of 1.9).  Entry bits: 0 / 1 exit mode entering in K /
+// V, [2, 4) / [4, 6) record ends, [6, 9) / [9, 12) boundary index (7: none), [12, 15) the
+// last NUL's index (7: none).
+template <bool MDBM>
+struct SpanTab {
+  uint16_t v[1024];
+  constexpr SpanTab() : v() {
+    for (uint32_t s = 0; s < 1024; ++s) {
+      uint32_t out = 0, nul = 7;
+      for (uint32_t m = 0; m < 2; ++m) {
+        uint32_t mode = m, cnt = 0, last = 7;
+        for (uint32_t i = 0; i < kEvCap; ++i) {
+          const uint32_t t = (s >> (2 * i)) & 3u;
+          if (t == 1u && mode == 1u) {  // a newline read in V ends the record
+            ++cnt;
+            last = i;
+            mode = 0;
+          } else if (MDBM ? t == 1u : (t == 2u && mode == 0u)) {  // the key's delimiter
+            last = i;
+            mode = 1;
+          }
+        }
+        out |= (mode << m) | (cnt << (2 + 2 * m)) | (last << (6 + 3 * m));
+      }
+      for (uint32_t i = 0; i < kEvCap; ++i)
+        if (((s >> (2 * i)) & 3u) == 3u) nul = i;
+      v[s] = (uint16_t)(out | (nul << 12));
+    }
+  }
+};
+__device__ const SpanTab<false> kSpanTabTsv{};
+__device__ const SpanTab<true> kSpanTabMdbm{};
+template <bool MDBM>
+__device__ inline LFn lfn_of_packed(uint64_t pk, uint32_t rel) {
+  static_assert(kEvCap == 5, "five 2-bit types index the table");
+  const uint32_t lo = (uint32_t)pk, hi = (uint32_t)(pk >> 32);
+  // types at bits 9 j + 7 of the word
+  const uint32_t s = ((lo >> 7) & 3u) | ((lo >> 14) & 0xCu) | ((lo >> 21) & 0x30u) | ((hi << 4) & 0xC0u) |
+                     ((hi >> 3) & 0x300u);
+  const uint32_t e = MDBM ? kSpanTabMdbm.v[s] : kSpanTabTsv.v[s];
+  auto p1 = [&](uint32_t i) { return i < kEvCap ? rel + ((uint32_t)(pk >> (9 * i)) & 127u) + 1u : 0u; };
+  return LFn{((e & 1u) ? kSelV : kSelK) | (((e & 2u) ? kSelV : kSelK) << 16), ((e >> 2) & 3u) | (((e >> 4) & 3u) << 16),
+             p1((e >> 6) & 7u) | (p1((e >> 9) & 7u) << 16), p1((e >> 12) & 7u)};
+}
+
 // Walk the candidate bytes of a span staged at `span`, calling f(offset, type) for each
 // (type 0 for a candidate that is no event: f must treat it as none).
 template <bool MDBM, class F>
@@ -837,8 +887,11 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       }
     }
   };
-  LFn acc = lfn_id();
-  for_events([&](uint32_t o, uint32_t t) { acc = lfn_push<MDBM>(acc, t, rel + o + 1); });
+  LFn acc = lfn_of_packed<MDBM>(pk, rel);  // (a span past the file: no events, the identity)
+  if (over) {  // more than kEvCap events (rare): from the file
+    acc = lfn_id();
+    for_events([&](uint32_t o, uint32_t t) { acc = lfn_push<MDBM>(acc, t, rel + o + 1); });
+  }
   LFn pre, agg;
   Scan(tmp).ExclusiveScan(acc, pre, lfn_id(), LCompose(), agg);
   const TState su = gapply(ein, tin);  // the state entering the unit
