@@ -829,9 +829,10 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   // The unit's records, staged in LDS and written out as consecutive 16-byte pieces across
   // the wave (round 4; round 3: each lane stored its own records' halves, 1.31x the
   // algorithmic bytes written).  A unit with more than kStageRecs records stores directly.
-  __shared__ uint64_t s_rec[kStageRecs * 4];  // key_off, key_len, val_off, val_len
-  __shared__ uint64_t s_h[kStageRecs * 2];    // h1, h2
-  __shared__ uint8_t s_fk[kStageRecs], s_fv[kStageRecs], s_fh[kStageRecs];  // which parts this unit wrote
+  // (row kStageRecs: the dump row of the branch-free walk)
+  __shared__ __attribute__((aligned(16))) uint64_t s_rec[(kStageRecs + 1) * 4];  // key_off, key_len, val_off, val_len
+  __shared__ __attribute__((aligned(16))) uint64_t s_h[(kStageRecs + 1) * 2];    // h1, h2
+  __shared__ uint8_t s_fk[kStageRecs + 1], s_fv[kStageRecs + 1], s_fh[kStageRecs + 1];  // which parts this unit wrote
   constexpr uint64_t HDR = MDBM ? kHdrRecs : 0;
   const uint64_t base = (uint64_t)blockIdx.x * kUnit;
   const uint64_t blk = blockIdx.x / kUnitsPerBlock;  // pass A's block
@@ -980,11 +981,41 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   // then the state by selects.  A field ends at its getline's delimiter (TSV: TAB for a
   // key, newline for a value; mdbm: newline for both) or at its first NUL; the delimiter
   // flips the mode, and a newline read in V ends the record.
+  // A staged unit (nearly all) takes the walk without branches (round 5): every event writes
+  // its record half and flag, to the dump row when no field of a record of this call ends
+  // there, and only a key pass A could not hash branches (to hash it from the file); the
+  // round-4 form branched on field ends, ~20 SALU per event of exec-mask bookkeeping.
+  const bool staged_u = __builtin_amdgcn_readfirstlane(staged ? 1 : 0) != 0;
+  typedef uint64_t u64x2a16 __attribute__((ext_vector_type(2)));
   for_events([&](uint32_t o, uint32_t t) {
     const uint64_t pos = base + rel + o;
     const bool nl = t == 1u, nul = t == 3u;
     const bool brk = MDBM ? nl : (s.m ? nl : t == 2u);  // the getline's delimiter
-    if (!nulf && (brk || nul)) {
+    const bool fe = !nulf && (brk || nul);             // a field's C string ends here
+    if (staged_u) {
+      const bool in = s.r >= HDR && s.r < lim;
+      const bool ke = fe && !s.m && in, ve = fe && s.m && in;
+      const uint32_t x = (uint32_t)(s.r - su.r);
+      const uint32_t xk = ke ? x : kStageRecs, xv = ve ? x : kStageRecs, xr = ve ? xv : xk;
+      *reinterpret_cast<u64x2a16*>(&s_rec[4 * xr + (ve ? 2u : 0u)]) = u64x2a16{s.fs, pos - s.fs};
+      s_fk[xk] = 1;
+      s_fv[xv] = 1;
+      if constexpr (MDBM)
+        if (fe && s.m && s.r == 2) val_end(pos, nul);  // the fifth header line's check (record 2 < HDR)
+      if constexpr (HASH) {
+        const uint64_t len = pos - s.fs;
+        const bool hit = j < kSlots && len <= kSpecLenMax && ((pk >> (48 + 8 * j)) & 0xFFu) == len;
+        const uint64_t raw = j == 0 ? sl_raw.x : sl_raw.y;
+        uint64_t a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
+        uint64_t c = pos > s.fs ? raw : a;
+        if (ke && !hit) {
+          if (s.fs <= pos && pos <= size) hash_cstr(f, s.fs, pos - s.fs, sp, a, c);
+          else a = c = 0;  // a state outside the file (never for correct states): wrong records, not a fault
+        }
+        *reinterpret_cast<u64x2a16*>(&s_h[2 * xk]) = u64x2a16{a, c};
+        s_fh[xk] = 1;
+      }
+    } else if (fe) {
       if (s.m)
         val_end(pos, nul);
       else
