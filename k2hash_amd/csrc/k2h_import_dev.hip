@@ -1008,12 +1008,8 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
         const uint64_t raw = j == 0 ? sl_raw.x : sl_raw.y;
         uint64_t a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
         uint64_t c = pos > s.fs ? raw : a;
-        if (ke && !hit) {
-          if (s.fs <= pos && pos <= size) hash_cstr(f, s.fs, pos - s.fs, sp, a, c);
-          else a = c = 0;  // a state outside the file (never for correct states): wrong records, not a fault
-        }
         *reinterpret_cast<u64x2a16*>(&s_h[2 * xk]) = u64x2a16{a, c};
-        s_fh[xk] = 1;
+        s_fh[xk] = ke && !hit ? 2 : 1;  // 2: hashed from the file after the walk
       }
     } else if (fe) {
       if (s.m)
@@ -1058,6 +1054,21 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     if (half ? s_fv[x] : s_fk[x])
       __builtin_nontemporal_store(u64x2{s_rec[2 * q], s_rec[2 * q + 1]},
                                   reinterpret_cast<u64x2*>(&recs[su.r + x - HDR].key_off + 2 * half));
+  }
+  // keys pass A did not hash (0.8 % on BASELINE-like files), from the file: after the walk
+  // (round 5), one lane per key and few live registers, instead of inside it, where the hash
+  // raised the walk's register count (70 VGPRs, 7 waves per SIMD) and serialised the misses
+  if constexpr (HASH) {
+    for (uint32_t x = threadIdx.x; x < nrec; x += 64)
+      if (s_fh[x] == 2) {
+        const uint64_t o = s_rec[4 * x], n = s_rec[4 * x + 1];
+        uint64_t a = 0, c = 0;
+        if (o <= size && n <= size - o) hash_cstr(f, o, n, sp, a, c);  // (else: a wrong state; wrong records, no fault)
+        s_h[2 * x] = a;
+        s_h[2 * x + 1] = c;
+        s_fh[x] = 1;
+      }
+    __syncthreads();
   }
   if constexpr (HASH)
     for (uint32_t x = threadIdx.x; x < nrec; x += 64)
