@@ -384,6 +384,32 @@ def test_fused_scan_prehash_many_unspeculated_keys(cuda, oracle):
 
 
 @pytest.mark.gpu
+def test_fused_scan_prehash_misses_hashed_after_the_walk(cuda):
+    """Round 5: pass B hashes the keys pass A did not (a third cut in a span, keys of 255
+    bytes or more) after its walk, one lane per key.  Runs of records whose keys are all
+    longer than a slot holds (every key a miss, ~25 per staged unit), runs of short records
+    (spans with three or more cuts, misses mixed with hits) and ordinary ones, over many
+    units: records and hashes == the host scan + the host prehash."""
+    import torch
+    rng = np.random.default_rng(31)
+    parts = []
+    for i in range(24000):
+        kind = (i // 400) % 3
+        if kind == 0:
+            klen, vlen = int(rng.integers(255, 400)), int(rng.integers(0, 30))
+        elif kind == 1:
+            klen, vlen = int(rng.integers(1, 6)), int(rng.integers(0, 6))
+        else:
+            klen, vlen = int(rng.integers(8, 65)), int(rng.integers(0, 201))
+        k = bytes(rng.integers(33, 127, klen, dtype=np.uint8))
+        v = bytes(rng.integers(32, 127, vlen, dtype=np.uint8))
+        parts.append(k + b"\t" + v + b"\n")
+    data = b"".join(parts)
+    f = torch.from_numpy(np.frombuffer(data, np.uint8).copy()).to(cuda)
+    _check_fused(f, data, "tsv", archive.import_scan(data, "tsv"), "long and dense keys")
+
+
+@pytest.mark.gpu
 def test_fused_scan_prehash_staged_and_direct_units(cuda):
     """Round 4: pass B stages an 8 KiB unit's records in LDS when it touches at most 96 of
     them and stores directly otherwise.  One file whose units fall on both sides of that
