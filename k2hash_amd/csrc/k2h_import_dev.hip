@@ -906,14 +906,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   __syncthreads();
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
   uint32_t j = 0;           // cut events of this span so far
-  // a key ended in this span whose record's value has not ended yet: its fields wait so
-  // the record is written whole (two 16-byte stores) when the value ends here too
-  uint64_t pk_r = ~0ull, pk_off = 0, pk_len = 0;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));  // recs: 8-byte aligned
-  auto flush_key = [&]() {
-    if (pk_r != ~0ull) *reinterpret_cast<u64x2*>(&recs[pk_r].key_off) = u64x2{pk_off, pk_len};
-    pk_r = ~0ull;
-  };
   auto key_end = [&](uint64_t e) {
     if (s.r < HDR || s.r >= lim) return;
     const uint64_t r = s.r - HDR;
@@ -922,11 +915,8 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       s_rec[4 * x] = s.fs;
       s_rec[4 * x + 1] = e - s.fs;
       s_fk[x] = 1;
-    } else {
-      flush_key();
-      pk_r = r;
-      pk_off = s.fs;
-      pk_len = e - s.fs;
+    } else {  // a unit with more records than the stage (rare): the key half straight out
+      *reinterpret_cast<u64x2*>(&recs[r].key_off) = u64x2{s.fs, e - s.fs};
     }
     if constexpr (HASH) {
       uint64_t a, c;
@@ -968,10 +958,6 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       s_rec[4 * x + 2] = s.fs;
       s_rec[4 * x + 3] = e - s.fs;
       s_fv[x] = 1;
-    } else if (pk_r == r) {
-      *reinterpret_cast<u64x2*>(&recs[r].key_off) = u64x2{pk_off, pk_len};
-      *reinterpret_cast<u64x2*>(&recs[r].val_off) = u64x2{s.fs, e - s.fs};
-      pk_r = ~0ull;
     } else {
       *reinterpret_cast<u64x2*>(&recs[r].val_off) = u64x2{s.fs, e - s.fs};
     }
@@ -1043,7 +1029,6 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       }
     }
   }
-  flush_key();
   if (!staged) return;
   __syncthreads();
   // the staged parts, consecutive lanes on consecutive 16-byte pieces (a record's key half
