@@ -65,8 +65,24 @@ __device__ inline void hash_cstr(const uint8_t* __restrict__ f, uint64_t off, ui
     const uint32_t m2 = p >= 12 ? 0u : p <= 8 ? ~0u : ~0u << (8 * (p - 8)), m3 = p <= 12 ? ~0u : ~0u << (8 * (p - 12));
     c.x &= m0, c.y &= m1, c.z &= m2, c.w &= m3;
     uint32_t lo = (uint32_t)sp.v[p], hi = (uint32_t)(sp.v[p] >> 32);
+    // chunks 1-3 loaded before any is hashed, later ones one ahead (round 5: one load per
+    // loop trip, each waited for in turn, cost the miss-heavy mdbm pass B a round trip per chunk)
+    uint4 c1 = c, c2 = c, c3 = c;
+    if (k > 1) c1 = ld16(c0 + 16);
+    if (k > 2) c2 = ld16(c0 + 32);
+    if (k > 3) c3 = ld16(c0 + 48);
     fnv_chunk16(lo, hi, c);
-    for (uint64_t q = 1; q < k; ++q) fnv_chunk16(lo, hi, ld16(c0 + 16 * q));
+    if (k > 1) fnv_chunk16(lo, hi, c1);
+    if (k > 2) fnv_chunk16(lo, hi, c2);
+    if (k > 3) {
+      uint4 nx = c3;
+      for (uint64_t q = 4; q < k; ++q) {
+        const uint4 cur = nx;
+        nx = ld16(c0 + 16 * q);
+        fnv_chunk16(lo, hi, cur);
+      }
+      fnv_chunk16(lo, hi, nx);
+    }
     raw = ((uint64_t)hi << 32) | lo;
   }
   h1 = raw * 1099511628211ULL;  // lib/k2hashfunc.cc:56
