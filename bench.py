@@ -16,8 +16,8 @@ Every rank's shard is checked against the reference's digests
 (tests/golden/digests.json, fixed32_1G chunks) outside the timed region.
 
 At N = 1 the line also carries secondary results (configs 3, 4 and 5, config 2 with the fused
-bucket index, RALLEDATA blobs, the k2himport TSV scan + prehash of a file in HBM, and the
-host-memory path) and a CPU baseline: the reference's own hash path (oracle/_ref),
+bucket index, RALLEDATA blobs, the k2himport TSV and mdbm scans + prehash of a file in HBM,
+and the host-memory path) and a CPU baseline: the reference's own hash path (oracle/_ref),
 timed on this host's cores.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config fixed32|csr|fixed4096|fixed32_1g|ralledata]
@@ -232,9 +232,10 @@ def cpu_baseline(keys_host, key_len: int, n: int) -> dict | None:
         if nall != cores else kbN
     if not (t1 and tN):
         return None
-    # the reported value: the faster of the box's CPU share and every listed CPU
-    use_all = bool(tall) and tall < tN
-    threads, t = (nall, tall) if use_all else (cores, tN)
+    # the reported value: the pass on the threads this process may use (the cgroup's CPU
+    # share); the pass over every CPU the OS lists only time-shares that quota and is kept
+    # as a sub-field
+    threads, t = cores, tN
     kb = {"hash_calls_per_thread": 1000000,
           "threads_1": {"seconds": kb1, "calls_per_s": 1e6 / kb1 if kb1 > 0 else None},
           f"threads_{cores}": {"seconds": kbN, "calls_per_s": cores * 1e6 / kbN if kbN > 0 else None}}
@@ -258,8 +259,8 @@ def cpu_baseline(keys_host, key_len: int, n: int) -> dict | None:
     return {
         "value": n / t, "unit": "key hashes/s", "cores": threads, "kind": kind,
         "sample": f"first {n} keys of the same {key_len}B workload (first {m1} at 1 thread), h1 only, "
-                  f"8 passes per run, best of 3 runs, on {threads} threads (best of the box's {cores}-CPU "
-                  f"share and all {nall} listed CPUs; reference lib/k2hashfunc.cc k2h_hash via dlsym)",
+                  f"8 passes per run, best of 3 runs, on {threads} threads (the box's {cores}-CPU share; "
+                  f"all {nall} listed CPUs in all_listed_cpus; reference lib/k2hashfunc.cc k2h_hash via dlsym)",
         "single_thread": m1 / t1,
         "cpu_share": {"threads": cores, "value": n / tN},
         "all_listed_cpus": {"threads": nall, "value": n / tall if tall else None},
@@ -455,10 +456,31 @@ def measure_gather(h, counts, step, gsteps: int, dist, dev, sync=lambda: None) -
 # --------------------------------------------------------------------------------------
 # Timing
 # --------------------------------------------------------------------------------------
-def timed(step, steps: int, warmup: int, warm_ms: float, world: int = 1, dist=None, dev=None):
+_ROCTX = []
+
+
+def _roctx():
+    """rocprofiler-sdk's roctx, loaded only when K2H_BENCH_MARKERS=1 (tools/profile_line.sh
+    runs the driver's own command under rocprofv3 --kernel-trace --marker-trace with it): the
+    timed region of every line entry becomes a named range, so each figure in the line is
+    recomputed from the kernels inside its range (tools/summarize_line_profile.py)."""
+    if not _ROCTX:
+        lib = None
+        if os.environ.get("K2H_BENCH_MARKERS") == "1":
+            import ctypes
+
+            lib = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+            lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+        _ROCTX.append(lib)
+    return _ROCTX[0]
+
+
+def timed(step, steps: int, warmup: int, warm_ms: float, world: int = 1, dist=None, dev=None,
+          label: str = "headline"):
     """W untimed launches, then warm up for >= warm_ms, then EXACTLY `steps` launches bracketed
     by barrier + synchronize.  Returns (wall seconds (max over ranks), average launch time from
-    one event pair on the launch stream, extra warm-up launches)."""
+    one event pair on the launch stream, extra warm-up launches).  With K2H_BENCH_MARKERS=1 the
+    synchronised timed region is the roctx range "timed:<label>"."""
     import torch
 
     for i in range(warmup):
@@ -475,6 +497,9 @@ def timed(step, steps: int, warmup: int, warm_ms: float, world: int = 1, dist=No
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
+    mk = _roctx()
+    if mk:
+        mk.roctxRangePushA(f"timed:{label}".encode())
     t0 = time.perf_counter()
     e0.record()
     for i in range(steps):
@@ -482,6 +507,8 @@ def timed(step, steps: int, warmup: int, warm_ms: float, world: int = 1, dist=No
     e1.record()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if mk:
+        mk.roctxRangePop()
     if distributed:
         dist.barrier()
     elapsed = t1 - t0
@@ -558,10 +585,11 @@ def secondary_csr(dev, steps, warm_ms, verify, cpu=False):
     nbytes = int(off[-1].item())
     data = batch.synth_bytes(nbytes, dev)
     h1 = torch.empty(n, dtype=torch.int64, device=dev)
-    wall, kern, _ = timed(lambda i: k2hash_amd.hash_csr(data, off, out=(h1, None)), steps, 3, warm_ms)
+    wall, kern, _ = timed(lambda i: k2hash_amd.hash_csr(data, off, out=(h1, None)), steps, 3, warm_ms,
+                          label="csr")
     algo = nbytes + 8 * n + 8 * (n + 1)
     model = sum(chunks_of(L) for L in range(lo, hi + 1)) / (hi - lo + 1) * FNV_OPS_PER_CHUNK * n / 64
-    res = {"workload": CONFIGS["csr"][3], "keys": n, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
+    res = {"workload": CONFIGS["csr"][3], "keys": n, "steps": steps, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
            "value": n * steps / wall, "unit": "key hashes/s", "roofline": roofline("csr", algo, kern, model, n)}
     if verify:
         res["verify"] = verify_chunks(h1, 0, _golden()["csr_8_256_64M"]["chunks"])
@@ -589,11 +617,12 @@ def secondary_fixed(name, dev, steps, warm_ms, verify, golden_name, cpu=False):
     n = n or KEYS_1G
     keys = batch.synth_bytes(n * L, dev)
     h1 = torch.empty(n, dtype=torch.int64, device=dev)
-    wall, kern, _ = timed(lambda i: k2hash_amd.hash_fixed(keys, L, out=(h1, None)), steps, 3, warm_ms)
+    wall, kern, _ = timed(lambda i: k2hash_amd.hash_fixed(keys, L, out=(h1, None)), steps, 3, warm_ms,
+                          label=name)
     algo = n * L + 8 * n
     model = n / 64 * chunks_of(L) * FNV_OPS_PER_CHUNK
     res = {"workload": desc + (" -- all 2^30 keys on one GPU" if name == "fixed32_1g" else ""), "keys": n,
-           "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3, "value": n * steps / wall,
+           "steps": steps, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3, "value": n * steps / wall,
            "unit": "key hashes/s", "key_gib_per_s": n * L * steps / wall / 2**30,
            "roofline": roofline(name, algo, kern, model, n)}
     if verify:
@@ -624,11 +653,12 @@ def secondary_index(dev, steps, warm_ms, verify):
     sets = [batch.synth_bytes(n * L, dev, byte_off=s * n * L) for s in range(2)]  # set 0 = the digest's keys
     out = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(3)]
     wall, kern, _ = timed(lambda i: batch.hash_fixed_index(sets[i % 2], L, g["cur_mask"], g["collision_mask"],
-                                                           out=(out[0], None, out[1], out[2])), steps, 3, warm_ms)
+                                                           out=(out[0], None, out[1], out[2])), steps, 3, warm_ms,
+                          label="fixed32_index")
     algo = n * L + 8 * n + 16 * n
     model = n / 64 * chunks_of(L) * FNV_OPS_PER_CHUNK
     res = {"workload": desc + " + fused bucket index (cur_mask 2^28-1, collision_mask 0xF)", "keys": n,
-           "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3, "value": n * steps / wall,
+           "steps": steps, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3, "value": n * steps / wall,
            "unit": "key hashes + bucket positions/s", "roofline": roofline("fixed32_index", algo, kern, model, n)}
     if verify:
         batch.hash_fixed_index(sets[0], L, g["cur_mask"], g["collision_mask"], out=(out[0], None, out[1], out[2]))
@@ -640,36 +670,69 @@ def secondary_index(dev, steps, warm_ms, verify):
     return res
 
 
-def secondary_ralledata(dev, steps, warm_ms, verify):
-    """SURVEY 8f row 2: RALLEDATA blobs (hash + subhash + lengths + key + value) for bench's
-    ralledata workload, one kernel per call; checked against tests/golden/ralledata_digest.json
-    (the oracle's layout restatement over the reference-pinned hash)."""
+def ralledata_set(dev, n: int, s: int, first: int = 0, world: int = 1, rank: int = 0):
+    """Input set s of bench's RALLEDATA workload for this rank: 8M records (keys 8-64 B,
+    values 0-256 B), key and value lengths from the records' global indices, bytes from
+    disjoint splitmix64 streams.  Set 0 of rank 0 is tests/golden/ralledata_digest.json's
+    workload.  Returns ((keys, key_off, vals, val_off), (blob, blob_off), total blob bytes);
+    the blob is zero-padded to whole 8-byte words (the digest is taken over u64 words)."""
     import torch
 
-    from k2hash_amd import batch, ralledata
+    from k2hash_amd import batch
 
-    _, n, ((klo, khi), (vlo, vhi)), desc = CONFIGS["ralledata"]
-    ko = batch.synth_offsets(n, dev, klo, khi)
-    vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7)
+    (klo, khi), (vlo, vhi) = CONFIGS["ralledata"][2]
+    base = first + s * world * n
+    ko = batch.synth_offsets(n, dev, klo, khi, first_key=base)
+    vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7, first_key=base)
     kb, vb = int(ko[-1].item()), int(vo[-1].item())
-    kd = batch.synth_bytes(kb, dev)
-    vd = batch.synth_bytes(vb, dev, byte_off=1 << 33)
+    kd = batch.synth_bytes(kb, dev, byte_off=s * (1 << 36) + rank * (1 << 34))
+    vd = batch.synth_bytes(vb, dev, byte_off=s * (1 << 36) + rank * (1 << 34) + (1 << 33))
     total = 80 * n + kb + vb
-    blob = torch.zeros((total + 7) // 8 * 8, dtype=torch.uint8, device=dev)  # zero pad: digest over u64 words
+    blob = torch.zeros((total + 7) // 8 * 8, dtype=torch.uint8, device=dev)
     boff = torch.empty(n + 1, dtype=torch.int64, device=dev)
-    wall, kern, _ = timed(lambda i: ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff, total=total),
-                          steps, 3, warm_ms)
-    algo = (kb + vb + 16 * (n + 1)) + (total + 8 * (n + 1))
+    return (kd, ko, vd, vo), (blob, boff), total
+
+
+def ralledata_algo_bytes(io) -> int:
+    """Minimal traffic of one build: key + value bytes and their offsets in, the blobs and
+    blob offsets out."""
+    (kd, ko, vd, vo) = io
+    n = ko.numel() - 1
+    kb, vb = kd.numel(), vd.numel()
+    return (kb + vb + 16 * (n + 1)) + (80 * n + kb + vb + 8 * (n + 1))
+
+
+def secondary_ralledata(dev, steps, warm_ms, verify):
+    """SURVEY 8f row 2: RALLEDATA blobs (hash + subhash + lengths + key + value) for bench's
+    ralledata workload, one kernel per call, two input sets rotated exactly as the standalone
+    `--config ralledata` run (the line's figure and the profile's are the same
+    code path); checked against tests/golden/ralledata_digest.json (the oracle's layout
+    restatement over the reference-pinned hash)."""
+    import torch
+
+    from k2hash_amd import ralledata
+
+    _, n, ((klo, khi), _v), desc = CONFIGS["ralledata"]
+    sets = [ralledata_set(dev, n, s) for s in range(2)]
+
+    def step(i):
+        (kd, ko, vd, vo), (blob, boff), total = sets[i % 2]
+        ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff, total=total)
+
+    wall, kern, _ = timed(step, steps, 3, warm_ms, label="ralledata")
+    algo = max(ralledata_algo_bytes(io) for io, _o, _t in sets)
+    total = sets[0][2]
     model = sum(chunks_of(L) for L in range(klo, khi + 1)) / (khi - klo + 1) * FNV_OPS_PER_CHUNK * n / 64
-    res = {"workload": desc, "records": n, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
+    res = {"workload": desc, "records": n, "steps": steps, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
            "value": n * steps / wall, "unit": "records/s", "blob_gb_per_s": total * steps / wall / 1e9,
-           "roofline": roofline("ralledata", algo, kern, model, n)}
+           "input_sets": 2, "roofline": roofline("ralledata", algo, kern, model, n)}
     if verify:
+        (_io, (blob, boff), total) = sets[0]  # written by step 18, untouched since
         g = json.loads((ROOT / "tests" / "golden" / "ralledata_digest.json").read_text())
         ok = g["n"] == n and g["bytes"] == total and digest_dev(blob.view(torch.int64), 0) == g["blob"] and \
             digest_dev(boff, 0) == g["blob_off"]
         res["verify"] = {"ok": ok, "against": "tests/golden/ralledata_digest.json"}
-    del ko, vo, kd, vd, blob, boff
+    del sets
     torch.cuda.empty_cache()
     return res
 
@@ -714,21 +777,90 @@ def secondary_import(dev, steps, warm_ms, verify):
     def step(i):
         out["r"] = archive.import_scan_prehash_device(data)
 
-    wall, kern, _ = timed(step, steps, 2, warm_ms)
+    wall, kern, _ = timed(step, steps, 2, warm_ms, label="import")
     algo = size + 32 * n + 16 * n  # the file once, the records, the two hashes
     model = sum(chunks_of(L) for L in range(IMPORT_KEY_LENS[0], IMPORT_KEY_LENS[1] + 1)) / \
         (IMPORT_KEY_LENS[1] - IMPORT_KEY_LENS[0] + 1) * FNV_OPS_PER_CHUNK * n / 64
     res = {"workload": f"{n} TSV records (keys 8-64 B, values 0-200 B, {size} B file in HBM) -> records + h1/h2",
-           "records": n, "file_bytes": size, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
+           "records": n, "file_bytes": size, "steps": steps, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
            "value": n * steps / wall, "unit": "records/s", "file_gb_per_s": size * steps / wall / 1e9,
            "roofline": roofline("import", algo, wall / steps, model, n)}
     if verify:
-        recs, h1, h2 = out["r"]
-        g = json.loads((ROOT / "tests" / "golden" / "import_digest.json").read_text())
-        cols = {"key_off": recs[:, 0], "key_len": recs[:, 1], "val_off": recs[:, 2], "val_len": recs[:, 3],
-                "h1": h1, "h2": h2}
-        ok = g["records"] == recs.shape[0] == n and all(digest_dev(v.contiguous(), 0) == g[k] for k, v in cols.items())
-        res["verify"] = {"ok": bool(ok), "against": "tests/golden/import_digest.json"}
+        res["verify"] = _import_verify(out["r"], "import_digest.json")
+    del data, out
+    torch.cuda.empty_cache()
+    return res
+
+
+MDBM_HDR = b"format=print\ntype=btree\nmdbm_pagesize=4096\nmdbm_pagecount=1\nHEADER=END\n"
+
+
+def import_mdbm_workload(dev):
+    """The import workload's 2^23 records in mdbm's print format (tests/k2himport.cc:95-117):
+    the five header lines, then a key line and a value line per record, built on the device
+    -- the file tests/golden/make_import_digest.py --mdbm builds on the host.  Returns the
+    file and each record's (key_off, key_len, val_off, val_len) by construction."""
+    import torch
+
+    from k2hash_amd import batch
+
+    n = IMPORT_N
+    kl = batch.synth_offsets(n, dev, *IMPORT_KEY_LENS, seed=batch.SEED_LENS + 11).diff()
+    vl = batch.synth_offsets(n, dev, *IMPORT_VAL_LENS, seed=batch.SEED_LENS + 13).diff()
+    h = len(MDBM_HDR)
+    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(kl + vl + 2, dim=0, out=off[1:])
+    off += h
+    data = batch.synth_bytes(int(off[-1].item()), dev, byte_off=IMPORT_BYTE_OFF)
+    data.remainder_(95).add_(32)
+    data[:h] = torch.frombuffer(bytearray(MDBM_HDR), dtype=torch.uint8).to(dev)
+    data[off[:-1] + kl] = 10
+    data[off[1:] - 1] = 10
+    exp = torch.stack([off[:-1], kl, off[:-1] + kl + 1, vl], dim=1)
+    return data, exp
+
+
+def _import_verify(out, golden: str) -> dict:
+    import torch  # noqa: F401
+
+    recs, h1, h2 = out
+    g = json.loads((ROOT / "tests" / "golden" / golden).read_text())
+    cols = {"key_off": recs[:, 0], "key_len": recs[:, 1], "val_off": recs[:, 2], "val_len": recs[:, 3],
+            "h1": h1, "h2": h2}
+    ok = g["records"] == recs.shape[0] == IMPORT_N and all(digest_dev(v.contiguous(), 0) == g[k]
+                                                           for k, v in cols.items())
+    return {"ok": bool(ok), "against": f"tests/golden/{golden}"}
+
+
+def secondary_import_mdbm(dev, steps, warm_ms, verify):
+    """SURVEY 8f row 3, mdbm form: k2himport's mdbm loop (tests/k2himport.cc:95-117: the
+    HEADER=END check, then key line / value line) over the import workload's records in
+    mdbm's print format, resident in HBM -> records + every key's h1 / h2, one call
+    (k2h_amd_import_scan_prehash_device, format mdbm).  Checked against
+    tests/golden/import_mdbm_digest.json (the tool's getline loop + the reference hash)."""
+    import torch
+
+    from k2hash_amd import archive
+
+    data, _exp = import_mdbm_workload(dev)
+    del _exp
+    n, size = IMPORT_N, data.numel()
+    out = {}
+
+    def step(i):
+        out["r"] = archive.import_scan_prehash_device(data, "mdbm")
+
+    wall, kern, _ = timed(step, steps, 2, warm_ms, label="import_mdbm")
+    algo = size + 32 * n + 16 * n
+    model = sum(chunks_of(L) for L in range(IMPORT_KEY_LENS[0], IMPORT_KEY_LENS[1] + 1)) / \
+        (IMPORT_KEY_LENS[1] - IMPORT_KEY_LENS[0] + 1) * FNV_OPS_PER_CHUNK * n / 64
+    res = {"workload": f"{n} mdbm records (key line 8-64 B, value line 0-200 B, {size} B file in HBM) -> "
+                       "records + h1/h2",
+           "records": n, "file_bytes": size, "steps": steps, "ms_per_step": wall / steps * 1e3, "kernel_ms": kern * 1e3,
+           "value": n * steps / wall, "unit": "records/s", "file_gb_per_s": size * steps / wall / 1e9,
+           "roofline": roofline("import_mdbm", algo, wall / steps, model, n)}
+    if verify:
+        res["verify"] = _import_verify(out["r"], "import_mdbm_digest.json")
     del data, out
     torch.cuda.empty_cache()
     return res
@@ -946,19 +1078,11 @@ def main():
         if kind == "fixed":
             sets.append((batch.synth_bytes(n * shape, dev, byte_off=base * shape), None))
             algo_bytes, key_bytes = n * shape + 8 * n, n * shape
-        elif kind == "ralledata":
-            (klo, khi), (vlo, vhi) = shape
-            ko = batch.synth_offsets(n, dev, klo, khi, first_key=base)
-            vo = batch.synth_offsets(n, dev, vlo, vhi, seed=batch.SEED_LENS + 7, first_key=base)
-            kb, vb = int(ko[-1].item()), int(vo[-1].item())
-            kd = batch.synth_bytes(kb, dev, byte_off=s * (1 << 36) + rank * (1 << 34))
-            vd = batch.synth_bytes(vb, dev, byte_off=s * (1 << 36) + rank * (1 << 34) + (1 << 33))
-            blob = torch.empty(80 * n + kb + vb, dtype=torch.uint8, device=dev)
-            boff = torch.empty(n + 1, dtype=torch.int64, device=dev)
-            sets.append(((kd, ko, vd, vo), (blob, boff)))
-            # minimal traffic: key + value bytes and their offsets in, blobs + blob offsets out
-            algo_bytes = max(algo_bytes, (kb + vb + 16 * (n + 1)) + (80 * n + kb + vb + 8 * (n + 1)))
-            key_bytes = max(key_bytes, kb)
+        elif kind == "ralledata":  # the same sets as secondary_ralledata (ralledata_set)
+            io, outb, tot = ralledata_set(dev, n, s, first, world, rank)
+            sets.append((io, outb + (tot,)))
+            algo_bytes = max(algo_bytes, ralledata_algo_bytes(io))
+            key_bytes = max(key_bytes, io[0].numel())
         elif strong:  # this rank's byte range of the one reference batch (byte stream offset = its first byte)
             off = batch.synth_offsets(last - first, dev, shape[0], shape[1], first_key=first)
             b0 = bs[rank]
@@ -987,8 +1111,8 @@ def main():
         keys, off = sets[i % nsets]
         if kind == "ralledata":
             from k2hash_amd import ralledata
-            (kd, ko, vd, vo), (blob, boff) = keys, off
-            ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff, total=blob.numel())
+            (kd, ko, vd, vo), (blob, boff, tot) = keys, off
+            ralledata.build_ralledata(kd, ko, vd, vo, out=blob, blob_off=boff, total=tot)
         elif args.index:
             h1, h2 = outs[i % nsets]
             k, c = idx[i % nsets]
@@ -1001,7 +1125,7 @@ def main():
         else:
             k2hash_amd.hash_csr(keys, off, second=args.second, out=outs[i % nsets])
 
-    elapsed, kern_s, extra = timed(step, args.steps, args.warmup, args.warm_ms, world, dist, dev)
+    elapsed, kern_s, extra = timed(step, args.steps, args.warmup, args.warm_ms, world, dist, dev, label="headline")
     total_keys = (total if strong else n * world) * args.steps
     value = total_keys / elapsed
 
@@ -1058,6 +1182,7 @@ def main():
                 "fixed32_index": secondary_index(dev, 20, 60.0, vf),
                 "ralledata": secondary_ralledata(dev, 20, 60.0, vf),
                 "import": secondary_import(dev, 10, 60.0, vf),
+                "import_mdbm": secondary_import_mdbm(dev, 10, 60.0, vf),
                 "host": secondary_host(dev),
             }
             cb = secondary["csr"].get("cpu_baseline")

@@ -42,6 +42,52 @@ uint64_t seed_for(uint32_t flags) {
 }
 
 // ---------------------------------------------------------------------------
+// Device gate (include/k2hash_amd.h: K2H_AMD_ENODEV = "no usable gfx950 device").  The
+// library carries gfx950 code objects only, so every entry point that launches checks the
+// device's architecture once (cached per device) and returns ENODEV before any launch on a
+// device without a gfx950 ISA.  K2H_AMD_TEST_ARCH, read once per process, replaces the name
+// the runtime reports: a test hook that lets a gfx950 box exercise the refusal.
+// ---------------------------------------------------------------------------
+constexpr int kMaxDevices = 64;
+std::atomic<int8_t> g_arch_ok[kMaxDevices];  // 0 unknown, 1 gfx950, -1 other
+
+int gate_device(int device) {
+  if (device < 0 || device >= kMaxDevices) return fail(K2H_AMD_EINVAL, "device index out of range");
+  int8_t s = g_arch_ok[device].load(std::memory_order_relaxed);
+  if (s == 0) {
+    static const char* forced = getenv("K2H_AMD_TEST_ARCH");
+    char name[256] = {0};
+    if (forced) {
+      snprintf(name, sizeof name, "%s", forced);
+    } else {
+      hipDeviceProp_t p;
+      hipError_t e = hipGetDeviceProperties(&p, device);
+      if (e != hipSuccess) return fail(K2H_AMD_ENODEV, "hipGetDeviceProperties", e);
+      snprintf(name, sizeof name, "%s", p.gcnArchName);
+    }
+    // gcnArchName is "gfx950" or "gfx950:sramecc+:xnack-": the processor name before ':'
+    s = (strncmp(name, "gfx950", 6) == 0 && (name[6] == 0 || name[6] == ':')) ? 1 : -1;
+    g_arch_ok[device].store(s, std::memory_order_relaxed);
+  }
+  if (s < 0) return fail(K2H_AMD_ENODEV, "device is not gfx950 (this library holds gfx950 code only)");
+  return K2H_AMD_OK;
+}
+
+// The caller's current device (device-pointer entry points launch there).
+int gate_current() {
+  int d = -1;
+  hipError_t e = hipGetDevice(&d);
+  if (e != hipSuccess) return fail(K2H_AMD_ENODEV, "no HIP device", e);
+  return gate_device(d);
+}
+
+#define K2H_GATE()                          \
+  do {                                      \
+    if (int gate_rc_ = gate_current())      \
+      return gate_rc_;                      \
+  } while (0)
+
+// ---------------------------------------------------------------------------
 // Parallel host copies for the staging pipeline.  One core's memcpy into pinned memory
 // runs at ~16 GB/s on the MI355X hosts, a third of PCIe (57 GB/s measured,
 // tools/host_rate.py), so staging copies are split over a small worker pool.  The pool
@@ -249,6 +295,7 @@ class DeviceGuard {
     hipError_t e = hipGetDeviceCount(&count);
     if (e != hipSuccess || count == 0) return fail(K2H_AMD_ENODEV, "no HIP device", e);
     if (device < 0 || device >= count || device >= 64) return fail(K2H_AMD_EINVAL, "device index out of range");
+    if (int rc = gate_device(device)) return rc;
     if ((e = hipGetDevice(&prev_)) != hipSuccess) return fail(K2H_AMD_EHIP, "hipGetDevice", e);
     if (prev_ != device && (e = hipSetDevice(device)) != hipSuccess) return fail(K2H_AMD_EHIP, "hipSetDevice", e);
     set_ = prev_ != device;
@@ -273,6 +320,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed(const void* keys, 
   if (n == 0) return K2H_AMD_OK;
   if (!h1) return fail(K2H_AMD_EINVAL, "h1 is NULL");
   if (key_len && n > UINT64_MAX / key_len) return fail(K2H_AMD_EINVAL, "n * key_len overflows");
+  K2H_GATE();
   hipError_t e = k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, (hipStream_t)stream);
   if (e != hipSuccess) return fail(K2H_AMD_EHIP, "launch_fixed", e);
   return K2H_AMD_OK;
@@ -283,6 +331,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr(const void* bytes, c
                                                             void* stream) {
   if (n == 0) return K2H_AMD_OK;
   if (!h1 || !offsets) return fail(K2H_AMD_EINVAL, "h1/offsets is NULL");
+  K2H_GATE();
   hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, (hipStream_t)stream);
   if (e != hipSuccess) return fail(K2H_AMD_EHIP, "launch_csr", e);
   return K2H_AMD_OK;
@@ -318,6 +367,7 @@ __attribute__((visibility("default"))) int k2h_amd_bucket_index(const uint64_t* 
   k2h::BucketParams bp;
   int rc = bucket_params(cur_mask, collision_mask, kindex, ckindex, bp);
   if (rc) return rc;
+  K2H_GATE();
   hipError_t e = k2h::launch_bucket_index(h1, n, bp, (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_bucket_index", e);
 }
@@ -333,6 +383,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed_index(const void* 
   k2h::BucketParams bp;
   int rc = bucket_params(cur_mask, collision_mask, kindex, ckindex, bp);
   if (rc) return rc;
+  K2H_GATE();
   hipError_t e =
       k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_fixed (index)", e);
@@ -348,6 +399,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_index(const void* by
   k2h::BucketParams bp;
   int rc = bucket_params(cur_mask, collision_mask, kindex, ckindex, bp);
   if (rc) return rc;
+  K2H_GATE();
   hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_csr (index)", e);
 }
@@ -383,6 +435,7 @@ __attribute__((visibility("default"))) int k2h_amd_bucket_index_table(const uint
   if (rc) return rc;
   bp.assigned = table->assigned;
   bp.found = table->assigned ? found : nullptr;
+  K2H_GATE();
   if ((rc = null_bitmap_fill(table, n, kindex, found, bp, stream))) return rc;
   hipError_t e = k2h::launch_bucket_index(h1, n, bp, (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_bucket_index (table)", e);
@@ -400,6 +453,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_fixed_index_table(
   if (rc) return rc;
   bp.assigned = table->assigned;
   bp.found = table->assigned ? found : nullptr;
+  K2H_GATE();
   if ((rc = null_bitmap_fill(table, n, kindex, found, bp, stream))) return rc;
   hipError_t e = k2h::launch_fixed(keys, key_len, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_fixed (table index)", e);
@@ -416,6 +470,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_csr_index_table(
   if (rc) return rc;
   bp.assigned = table->assigned;
   bp.found = table->assigned ? found : nullptr;
+  K2H_GATE();
   if ((rc = null_bitmap_fill(table, n, kindex, found, bp, stream))) return rc;
   hipError_t e = k2h::launch_csr(bytes, offsets, n, seed_for(flags), h1, h2, (hipStream_t)stream, &bp);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_csr (table index)", e);
@@ -536,6 +591,7 @@ __attribute__((visibility("default"))) int k2h_amd_hash_ranges(const void* base,
                                                                uint64_t* h2, uint32_t flags, void* stream) {
   if (n == 0) return K2H_AMD_OK;
   if (!h1 || !starts || !lens || !base) return fail(K2H_AMD_EINVAL, "NULL base/starts/lens/h1");
+  K2H_GATE();
   hipError_t e = k2h::launch_ranges(base, starts, lens, n, seed_for(flags), (flags & K2H_AMD_FLAG_CSTR) != 0, h1, h2,
                                     (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_ranges", e);
@@ -547,6 +603,7 @@ __attribute__((visibility("default"))) int k2h_amd_import_scan_device(const void
                                                                       uint64_t* count, void* stream) {
   if (!count || (size && !file) || (format != K2H_AMD_IMPORT_TSV && format != K2H_AMD_IMPORT_MDBM))
     return fail(K2H_AMD_EINVAL, "import_scan_device: NULL count/file or bad format");
+  if (size) K2H_GATE();  // an empty file has no records and needs no device
   hipError_t e = hipSuccess;
   int rc = k2h::launch_import_scan(file, size, format, recs, cap, count, (hipStream_t)stream, &e);
   if (rc == K2H_AMD_EHIP) return fail(rc, "launch_import_scan", e);
@@ -559,6 +616,7 @@ __attribute__((visibility("default"))) int k2h_amd_import_scan_prehash_device(
   if (!count || (size && !file) || (format != K2H_AMD_IMPORT_TSV && format != K2H_AMD_IMPORT_MDBM))
     return fail(K2H_AMD_EINVAL, "import_scan_prehash_device: NULL count/file or bad format");
   if (recs && cap && !h1) return fail(K2H_AMD_EINVAL, "import_scan_prehash_device: NULL h1");
+  if (size) K2H_GATE();  // an empty file has no records and needs no device
   hipError_t e = hipSuccess;
   int rc = k2h::launch_import_scan(file, size, format, recs, cap, count, (hipStream_t)stream, &e, h1, h2,
                                    seed_for(flags));
@@ -571,6 +629,7 @@ __attribute__((visibility("default"))) int k2h_amd_import_prehash(const void* fi
                                                                   uint32_t flags, void* stream) {
   if (n == 0) return K2H_AMD_OK;
   if (!file || !recs || !h1) return fail(K2H_AMD_EINVAL, "import_prehash: NULL file/recs/h1");
+  K2H_GATE();
   hipError_t e = k2h::launch_import_prehash(file, size, recs, n, seed_for(flags), h1, h2, (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "launch_import_prehash", e);
 }
@@ -592,6 +651,7 @@ __attribute__((visibility("default"))) int k2h_amd_build_ralledata(
   if (n && !out) return fail(K2H_AMD_EINVAL, "out is NULL");
   if ((val_off && !vals) || (skey_off && !skeys) || (attr_off && !attrs))
     return fail(K2H_AMD_EINVAL, "segment offsets without segment bytes");
+  K2H_GATE();
   k2h::RalleInputs in;
   in.keys = (const uint8_t*)keys;
   in.koff = key_off;
@@ -683,6 +743,7 @@ __attribute__((visibility("default"))) const char* k2h_amd_strerror(int code) {
 __attribute__((visibility("default"))) int k2h_amd_synth_bytes(void* out, uint64_t nbytes, uint64_t seed,
                                                                uint64_t byte_off, void* stream) {
   if (nbytes && !out) return fail(K2H_AMD_EINVAL, "out is NULL");
+  K2H_GATE();
   hipError_t e = k2h::launch_synth_bytes((uint8_t*)out, nbytes, seed, byte_off, (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "synth_bytes", e);
 }
@@ -692,6 +753,7 @@ __attribute__((visibility("default"))) int k2h_amd_synth_lengths(uint32_t* lens,
                                                                  uint32_t max_len, void* stream) {
   if (n && !lens) return fail(K2H_AMD_EINVAL, "lens is NULL");
   if (max_len < min_len) return fail(K2H_AMD_EINVAL, "max_len < min_len");
+  K2H_GATE();
   hipError_t e = k2h::launch_synth_lengths(lens, n, seed, first_key, min_len, max_len, (hipStream_t)stream);
   return e == hipSuccess ? K2H_AMD_OK : fail(K2H_AMD_EHIP, "synth_lengths", e);
 }

@@ -14,9 +14,10 @@
 // before each getline, C-string key / value bytes in hex, the two hashes) or an error.
 //
 //   gen_import tsv|mdbm <file>
-//   gen_import tsv-digest <file>   the TSV loop's records and hashes as order-sensitive
-//                                  digests {xor, sum, sum of v * (2i + 1)} per field (the
-//                                  bench's 8M-record workload, tests/golden/make_import_digest.py)
+//   gen_import tsv-digest|mdbm-digest <file>
+//                                  the loop's records and hashes as order-sensitive digests
+//                                  {xor, sum, sum of v * (2i + 1)} per field (the bench's
+//                                  8M-record workloads, tests/golden/make_import_digest.py)
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -44,14 +45,28 @@ struct Digest {  // oracle_digest (oracle/fnv_oracle.c), accumulated one value a
   }
 };
 
-static int tsv_digest(std::ifstream& is) {
+// The loops of tests/k2himport.cc:81-86 (TSV) and :104-113 (mdbm, after the header check of
+// :95-103) with every record folded into digests instead of printed.
+static int loop_digest(std::ifstream& is, bool tsv) {
   Digest d[6];
   uint64_t n = 0;
   std::string key, value;
-  for (;;) {  // the loop of tests/k2himport.cc:81-86
+  if (!tsv) {
+    std::string hdr[5];
+    for (int i = 0; i < 5; ++i) std::getline(is, hdr[i]);
+    if (hdr[4] != "HEADER=END") {
+      printf("{\"format\": \"mdbm\", \"error\": true}\n");
+      return 0;
+    }
+  }
+  for (;;) {
     long long koff = (long long)is.tellg();
-    if (!std::getline(is, key, '\t')) break;
-    if (is.eof()) break;
+    if (tsv) {
+      if (!std::getline(is, key, '\t')) break;
+      if (is.eof()) break;
+    } else if (!std::getline(is, key)) {
+      break;
+    }
     long long voff = (long long)is.tellg();
     std::getline(is, value);
     const char* kc = key.c_str();
@@ -65,7 +80,7 @@ static int tsv_digest(std::ifstream& is) {
     ++n;
   }
   static const char* names[6] = {"key_off", "key_len", "val_off", "val_len", "h1", "h2"};
-  printf("{\"format\": \"tsv\", \"records\": %llu", (unsigned long long)n);
+  printf("{\"format\": \"%s\", \"records\": %llu", tsv ? "tsv" : "mdbm", (unsigned long long)n);
   for (int k = 0; k < 6; ++k) {
     printf(", ");
     d[k].print(names[k]);
@@ -76,16 +91,16 @@ static int tsv_digest(std::ifstream& is) {
 
 int main(int argc, char** argv) {
   if (argc != 3) {
-    fprintf(stderr, "usage: gen_import tsv|mdbm|tsv-digest <file>\n");
+    fprintf(stderr, "usage: gen_import tsv|mdbm|tsv-digest|mdbm-digest <file>\n");
     return 2;
   }
-  if (strcmp(argv[1], "tsv-digest") == 0) {
+  if (strcmp(argv[1], "tsv-digest") == 0 || strcmp(argv[1], "mdbm-digest") == 0) {
     std::ifstream is(argv[2], std::ios::binary);
     if (!is) {
       fprintf(stderr, "cannot open %s\n", argv[2]);
       return 2;
     }
-    return tsv_digest(is);
+    return loop_digest(is, argv[1][0] == 't');
   }
   const bool tsv = strcmp(argv[1], "tsv") == 0;
   std::ifstream is(argv[2], std::ios::binary);

@@ -9,7 +9,11 @@ generators): 2^23 records "key TAB value NEWLINE", key lengths 8-64 and value le
 0-200 from the synthetic length streams (seeds SEED_LENS + 11 / + 13), bytes from the
 synthetic byte stream at byte offset 2^34 mapped to printable ASCII (32 + b % 95).
 
-  make -C oracle ref && python tests/golden/make_import_digest.py
+The mdbm form (--mdbm, tests/golden/import_mdbm_digest.json; bench.py secondary
+"import_mdbm"): the same records in mdbm's print format (tests/k2himport.cc:95-117), the
+five header lines first, key and value each on their own line.
+
+  make -C oracle ref && python tests/golden/make_import_digest.py [--mdbm]
 """
 import json
 import os
@@ -30,32 +34,44 @@ KEY_LENS, VAL_LENS = (8, 64), (0, 200)
 BYTE_OFF = 1 << 34
 
 
-def build(n: int = N) -> np.ndarray:
+MDBM_HDR = b"format=print\ntype=btree\nmdbm_pagesize=4096\nmdbm_pagecount=1\nHEADER=END\n"
+
+
+def build(n: int = N, mdbm: bool = False) -> np.ndarray:
+    """The TSV file, or (mdbm) the same records in mdbm's print format: the five header
+    lines, then per record a key line and a value line (the TAB becomes a newline)."""
     kl = np.diff(oracle.gen_offsets(n, *KEY_LENS, seed=SEED_LENS + 11)).astype(np.int64)
     vl = np.diff(oracle.gen_offsets(n, *VAL_LENS, seed=SEED_LENS + 13)).astype(np.int64)
-    off = np.concatenate([[0], np.cumsum(kl + vl + 2)])
+    h = len(MDBM_HDR) if mdbm else 0
+    off = np.concatenate([[0], np.cumsum(kl + vl + 2)]) + h
     data = oracle.gen_bytes(int(off[-1]), byte_off=BYTE_OFF)
     data = (data % 95 + 32).astype(np.uint8)
-    data[off[:-1] + kl] = 9
+    if mdbm:
+        data[:h] = np.frombuffer(MDBM_HDR, dtype=np.uint8)
+    data[off[:-1] + kl] = 10 if mdbm else 9
     data[off[1:] - 1] = 10
     return data
 
 
 def main():
+    mdbm = "--mdbm" in sys.argv[1:]
     gen = ROOT / "oracle" / "_ref" / "gen_import"
-    data = build()
-    with tempfile.NamedTemporaryFile(suffix=".tsv", delete=False) as t:
+    data = build(mdbm=mdbm)
+    with tempfile.NamedTemporaryFile(suffix=".mdbm" if mdbm else ".tsv", delete=False) as t:
         t.write(data.tobytes())
     try:
-        out = json.loads(subprocess.run([str(gen), "tsv-digest", t.name], check=True, capture_output=True,
-                                        text=True).stdout)
+        out = json.loads(subprocess.run([str(gen), "mdbm-digest" if mdbm else "tsv-digest", t.name], check=True,
+                                        capture_output=True, text=True).stdout)
     finally:
         os.unlink(t.name)
-    out.update({"generator": "tests/golden/make_import_digest.py (oracle/_ref/gen_import tsv-digest: "
-                             "k2himport's getline loop + the reference hash)",
+    out.update({"generator": f"tests/golden/make_import_digest.py{' --mdbm' if mdbm else ''} (oracle/_ref/gen_import "
+                             f"{'mdbm' if mdbm else 'tsv'}-digest: k2himport's getline loop + the reference hash)",
                 "bytes": int(data.size), "key_lens": KEY_LENS, "val_lens": VAL_LENS,
                 "seeds": {"key_lens": SEED_LENS + 11, "val_lens": SEED_LENS + 13, "bytes_offset": BYTE_OFF}})
-    (Path(__file__).resolve().parent / "import_digest.json").write_text(json.dumps(out, indent=1) + "\n")
+    if mdbm:
+        out["header"] = MDBM_HDR.decode()
+    name = "import_mdbm_digest.json" if mdbm else "import_digest.json"
+    (Path(__file__).resolve().parent / name).write_text(json.dumps(out, indent=1) + "\n")
     print(json.dumps(out))
 
 

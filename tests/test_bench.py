@@ -225,6 +225,21 @@ def test_cpu_baseline_workload_csr_and_fixed(oracle):
     assert bench.cpu_baseline_workload("fixed", keys, None, 4096, 8, 64, bad)["digest_matches_gpu"] is False
 
 
+def test_cpu_baseline_cores_is_the_process_share(oracle):
+    """the headline cpu_baseline is labelled by what this process may use
+    (affinity, cgroup quota, OMP_NUM_THREADS), and its value is that pass's; the pass over
+    every listed CPU stays a sub-field."""
+    sys.path.insert(0, str(ROOT))
+    import bench
+
+    keys = oracle.gen_bytes(32 * 20000)
+    r = bench.cpu_baseline(keys, 32, 20000)
+    cores = bench.usable_cores(bench.host_info())
+    assert r["cores"] == cores == r["cpu_share"]["threads"]
+    assert r["value"] == r["cpu_share"]["value"]
+    assert r["all_listed_cpus"]["threads"] == (os.cpu_count() or cores)
+
+
 @pytest.mark.gpu
 def test_bench_csr_two_ranks_one_batch_cut_by_bytes():
     """bench.py --config csr at N = 2 (two ranks sharing cuda:0 over gloo)

@@ -279,6 +279,54 @@ def test_bench_import_workload_digest(cuda):
 
 
 @pytest.mark.gpu
+def test_bench_import_mdbm_workload_digest(cuda):
+    """bench.py's import_mdbm secondary (VERDICT r5 #4): the same 8M records in mdbm's print
+    format, built on the device, scanned and prehashed in one call, equal k2himport's mdbm
+    loop + the reference hash over the same file (tests/golden/import_mdbm_digest.json,
+    make_import_digest.py --mdbm); the records also equal the generator's own layout."""
+    import sys
+
+    import torch
+
+    sys.path.insert(0, str(GOLDEN.parents[1]))
+    import bench
+
+    data, exp = bench.import_mdbm_workload(cuda)
+    recs, h1, h2 = archive.import_scan_prehash_device(data, "mdbm")
+    torch.cuda.synchronize()
+    g = json.loads((GOLDEN / "import_mdbm_digest.json").read_text())
+    assert g["bytes"] == data.numel() and g["records"] == recs.shape[0] == bench.IMPORT_N
+    assert torch.equal(recs, exp)
+    cols = {"key_off": recs[:, 0], "key_len": recs[:, 1], "val_off": recs[:, 2], "val_len": recs[:, 3], "h1": h1,
+            "h2": h2}
+    for k, v in cols.items():
+        assert bench.digest_dev(v.contiguous(), 0) == g[k], k
+
+
+def test_mdbm_digest_fixture_is_the_generators_file(oracle):
+    """The mdbm bench fixture's file is the TSV workload's records with each TAB a newline
+    after mdbm's five header lines (make_import_digest.build, the host twin of
+    bench.import_mdbm_workload); checked here on a 2000-record prefix against the
+    reference loop restated by the host scanner."""
+    import sys
+
+    sys.path.insert(0, str(GOLDEN))
+    import make_import_digest as mk
+
+    t = mk.build(2000)
+    m = mk.build(2000, mdbm=True)
+    h = len(mk.MDBM_HDR)
+    assert m[:h].tobytes() == mk.MDBM_HDR and m.size == t.size + h
+    assert (m[h:] == 10).sum() == 2 * 2000 and (t == 9).sum() == 2000
+    recs = archive.import_scan(m.tobytes(), "mdbm")
+    kl = np.diff(oracle.gen_offsets(2000, *mk.KEY_LENS, seed=mk.SEED_LENS + 11)).astype(np.int64)
+    vl = np.diff(oracle.gen_offsets(2000, *mk.VAL_LENS, seed=mk.SEED_LENS + 13)).astype(np.int64)
+    koff = h + np.concatenate([[0], np.cumsum(kl + vl + 2)])[:-1]
+    assert recs.size == 2000
+    assert (recs["key_off"] == koff).all() and (recs["key_len"] == kl).all() and (recs["val_len"] == vl).all()
+
+
+@pytest.mark.gpu
 def test_device_scan_over_4gib_tile_scan_runs(cuda):
     """A TSV file above 4 GiB (bench's 1.16 GB workload four times over: 282,643 blocks of
     16 KiB, 553 tiles): the tile-level entry-state scan runs its long-run form (more than

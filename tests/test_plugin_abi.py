@@ -189,6 +189,72 @@ def test_host_api_null_buffers_without_gpu():
     assert rc == 0 and not h1.any() and not h2.any()
 
 
+_GATE_CHILD = r"""
+import ctypes, json, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+from k2hash_amd import _native
+lib = _native.batch_lib()
+res = {}
+keys = np.arange(320, dtype=np.uint8)
+h1 = np.full(10, 7, np.uint64)
+# host path: the device gate runs before any staging or launch
+res["host"] = lib.k2h_amd_hash_fixed_host(ctypes.c_void_p(keys.ctypes.data), 32, 10,
+                                          ctypes.c_void_p(h1.ctypes.data), None, 0, 0)
+res["host_untouched"] = bool((h1 == 7).all())
+if sys.argv[2] == "gpu":
+    import torch
+    d = torch.arange(320, dtype=torch.uint8, device="cuda")
+    o = torch.full((10,), 7, dtype=torch.int64, device="cuda")
+    p = lambda t: ctypes.c_void_p(t.data_ptr())
+    res["fixed"] = lib.k2h_amd_hash_fixed(p(d), 32, 10, p(o), None, 0, None)
+    off = torch.arange(0, 330, 32, dtype=torch.int64, device="cuda").clamp_(max=320)
+    res["csr"] = lib.k2h_amd_hash_csr(p(d), p(off), 10, p(o), None, 0, None)
+    res["synth"] = lib.k2h_amd_synth_bytes(p(d), 320, 1, 0, None)
+    torch.cuda.synchronize()
+    res["device_untouched"] = bool((o == 7).all().item()) and bool((d == torch.arange(320, dtype=torch.uint8,
+                                                                                        device="cuda")).all().item())
+res["msg"] = lib.k2h_amd_strerror(-4).decode()
+print(json.dumps(res))
+"""
+
+
+def _gate_child(arch, mode):
+    env = dict(os.environ)
+    env.pop("K2H_AMD_TEST_ARCH", None)
+    if arch:
+        env["K2H_AMD_TEST_ARCH"] = arch
+    out = subprocess.run([os.sys.executable, "-c", _GATE_CHILD, str(ROOT), mode], capture_output=True, text=True,
+                         env=env, timeout=300)
+    assert out.returncode == 0, out.stderr[-2000:]
+    import json
+    return json.loads(out.stdout.strip().splitlines()[-1])
+
+
+def test_device_gate_refuses_non_gfx950():
+    """include/k2hash_amd.h: K2H_AMD_ENODEV = "no usable gfx950 device".  The test hook
+    K2H_AMD_TEST_ARCH stands in for the runtime's gcnArchName; on this GPU-less host the
+    gate refuses at hipGetDevice already.  Either way: ENODEV, and no launch or staging
+    touched the output."""
+    r = _gate_child("gfx942", "cpu")
+    assert r["host"] == _native.K2H_AMD_ENODEV and r["host_untouched"], r
+
+
+@pytest.mark.gpu
+def test_device_gate_on_gpu():
+    """On the gfx950 box: the forced non-gfx950 name makes every launching entry point
+    (device and host forms) return ENODEV before any launch -- the device output and the
+    input keep their bytes -- and the real name passes the gate."""
+    r = _gate_child("gfx942:sramecc+:xnack-", "gpu")
+    assert r["host"] == r["fixed"] == r["csr"] == r["synth"] == _native.K2H_AMD_ENODEV, r
+    assert r["host_untouched"] and r["device_untouched"] and "gfx950" in r["msg"], r
+    ok = _gate_child(None, "gpu")
+    assert ok["host"] == ok["fixed"] == ok["csr"] == ok["synth"] == _native.K2H_AMD_OK, ok
+    assert not ok["device_untouched"]  # the hashes were written
+    near = _gate_child("gfx9500", "gpu")  # a longer processor name is not gfx950
+    assert near["fixed"] == _native.K2H_AMD_ENODEV, near
+
+
 def test_python_mirror_scalar():
     assert k2hash_amd.k2h_hash(b"KEY-0000000000000000\0") == 0x0b2bb3288cdb4d49
     assert k2hash_amd.k2h_second_hash(b"KEY-0000000000000000\0") == 0x1bfb06d77c7f9f13

@@ -36,29 +36,8 @@ def _verify(out):
     return g["records"] == recs.shape[0] and all(bench.digest_dev(v.contiguous(), 0) == g[k] for k, v in cols.items())
 
 
-MDBM_HDR = b"format=print\ntype=btree\nmdbm_pagesize=4096\nmdbm_pagecount=1\nHEADER=END\n"
-
-
 def mdbm_workload(dev):
-    """The same 2^23 records as bench.import_workload in mdbm's print format (a key line and
-    a value line per record after the five header lines, tests/k2himport.cc:95-117), built
-    on the device; returns the file and each record's expected (key_off, key_len, val_off,
-    val_len)."""
-    from k2hash_amd import batch
-    n = bench.IMPORT_N
-    kl = batch.synth_offsets(n, dev, *bench.IMPORT_KEY_LENS, seed=batch.SEED_LENS + 11).diff()
-    vl = batch.synth_offsets(n, dev, *bench.IMPORT_VAL_LENS, seed=batch.SEED_LENS + 13).diff()
-    h = len(MDBM_HDR)
-    off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    torch.cumsum(kl + vl + 2, dim=0, out=off[1:])
-    off += h
-    data = batch.synth_bytes(int(off[-1].item()), dev, byte_off=bench.IMPORT_BYTE_OFF)
-    data.remainder_(95).add_(32)
-    data[:h] = torch.frombuffer(bytearray(MDBM_HDR), dtype=torch.uint8).to(dev)
-    data[off[:-1] + kl] = 10
-    data[off[1:] - 1] = 10
-    exp = torch.stack([off[:-1], kl, off[:-1] + kl + 1, vl], dim=1)
-    return data, exp
+    return bench.import_mdbm_workload(dev)
 
 
 def verify_mdbm(out, data, exp):
