@@ -1,0 +1,169 @@
+#!/usr/bin/env python3
+"""Lab A/B and phase clocks for the CSR kernel (BASELINE config 3: 64M keys of 8-256 B).
+
+  python tools/lab_csr.py --variants 0 1 [--reps 5 --launches 20] [--phases out.json]
+
+Variant 0 is the product launch (launch_csr_tile), 1 the product kernel with phase clocks
+(tools/lab/src/lab_csr_clock.inc), 2+ this round's experiments.  Every variant's hashes
+are checked against the reference's digests (tests/golden/digests.json csr_8_256_64M)
+before any timing; timings are interleaved, one event pair per batch of launches.
+--phases: analyse variant 1's clock records (per-wave phase durations, per-SIMD overlap of
+hash walks) and write them as JSON."""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import statistics
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+import bench  # noqa: E402  (digest helpers)
+
+_p, _u64 = ctypes.c_void_p, ctypes.c_uint64
+PHASES = ["setup_offsets", "dma_issue", "sort", "dma_wait", "walk", "stores"]
+
+
+def lab_lib():
+    lib = ctypes.CDLL(str(ROOT / "tools" / "lab" / "libk2hash_lab.so"))
+    lib.k2h_lab_csr.restype = ctypes.c_int
+    lib.k2h_lab_csr.argtypes = [ctypes.c_int, _p, _p, _u64, _p, _p, _p]
+    return lib
+
+
+def union_len(iv):
+    """Total length covered by intervals [(a, b)], and the length covered twice or more."""
+    ev = sorted([(a, 1) for a, b in iv] + [(b, -1) for a, b in iv])
+    one = two = 0
+    depth, last = 0, None
+    for t, d in ev:
+        if last is not None:
+            if depth >= 1:
+                one += t - last
+            if depth >= 2:
+                two += t - last
+        depth += d
+        last = t
+    return one, two
+
+
+def analyse(clk, n_blocks):
+    import numpy as np
+
+    r = clk.reshape(n_blocks * 4, 16).astype(np.int64)
+    T = np.stack([r[:, 0], r[:, 1], r[:, 2], r[:, 3], r[:, 4], r[:, 5], r[:, 6]], axis=1)
+    hw, xcc, m0, m1, smax, ssum = r[:, 7], r[:, 8], r[:, 9], r[:, 10], r[:, 11], r[:, 12]
+    valid = T[:, 0] != 0
+    T, hw, xcc, m0, m1, smax, ssum = (a[valid] for a in (T, hw, xcc, m0, m1, smax, ssum))
+    T = ((T - T[0, 0] + (1 << 31)) & 0xFFFFFFFF) - (1 << 31)  # low 32 bits of the counter: unwrap
+    T = (T - T[:, 0].min()) * 10  # 100 MHz realtime -> ns from the first wave's start
+    d = np.diff(T, axis=1)
+    span = int(T[:, 6].max() - T[:, 0].min())
+    res = {"waves": int(valid.sum()), "kernel_span_ns": span,
+           "phase_ns_per_wave": {p: {"mean": float(d[:, i].mean()), "median": float(np.median(d[:, i])),
+                                     "p90": float(np.percentile(d[:, i], 90))} for i, p in enumerate(PHASES)},
+           "phase_share_of_wave_time": {p: float(d[:, i].sum() / d.sum()) for i, p in enumerate(PHASES)}}
+    walk_ns = d[:, 4]
+    cyc = (m1 - m0) & 0xFFFFFFFF
+    ok = walk_ns > 0
+    res["walk"] = {"ns_per_step_mean": float((walk_ns[ok] / np.maximum(smax[ok], 1)).mean()),
+                   "clock_mhz_mean": float((cyc[ok] / walk_ns[ok] * 1e3).mean()),
+                   "steps_max_mean": float(smax.mean()), "lane_fill": float(ssum.sum() / (64 * smax.sum()))}
+    simd = (xcc << 16) | ((hw >> 4) & 0xFFF)  # xcc | se,sh,cu,simd bits of HW_ID
+    cu = (xcc << 16) | ((hw >> 8) & 0xFF)
+    res["simds_seen"] = int(len(np.unique(simd)))
+    res["cus_seen"] = int(len(np.unique(cu)))
+    # per SIMD: time with >= 1 / >= 2 waves walking, and with >= 1 wave resident at all
+    one = two = live = 0
+    order = np.argsort(simd, kind="stable")
+    s_sorted = simd[order]
+    cuts = np.flatnonzero(np.diff(s_sorted)) + 1
+    for grp in np.split(order, cuts):
+        o, t = union_len([(int(T[i, 4]), int(T[i, 5])) for i in grp])
+        one += o
+        two += t
+        live += union_len([(int(T[i, 0]), int(T[i, 6])) for i in grp])[0]
+    nsimd = len(cuts) + 1
+    res["simd_time"] = {"span_x_simds_ns": span * nsimd, "walking_ge1": one / (span * nsimd),
+                        "walking_ge2": two / (span * nsimd), "resident_ge1": live / (span * nsimd)}
+    # the tail: when the last block starts / when SIMDs run out of work
+    res["last_start_ns"] = int(T[:, 0].max())
+    res["first_end_of_last_generation_ns"] = int(np.percentile(T[:, 6], 99))
+    return res
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", nargs="+", type=int, required=True)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--launches", type=int, default=20)
+    ap.add_argument("--warm-ms", type=float, default=200.0)
+    ap.add_argument("--phases", default="")
+    args = ap.parse_args()
+
+    import time
+
+    import torch
+
+    from k2hash_amd import batch
+
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    lib = lab_lib()
+    sh = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    n, (lo, hi) = bench.CONFIGS["csr"][1], bench.CONFIGS["csr"][2]
+    off = batch.synth_offsets(n, dev, lo, hi)
+    data = batch.synth_bytes(int(off[-1].item()), dev)
+    h1 = torch.empty(n, dtype=torch.int64, device=dev)
+    nblk = (n + 511) // 512
+    clk = torch.zeros(nblk * 4 * 16, dtype=torch.int32, device=dev)
+    chunks = bench._golden()["csr_8_256_64M"]["chunks"]
+
+    def run(v):
+        rc = lib.k2h_lab_csr(v, ctypes.c_void_p(data.data_ptr()), ctypes.c_void_p(off.data_ptr()), n,
+                             ctypes.c_void_p(h1.data_ptr()), ctypes.c_void_p(clk.data_ptr()), sh)
+        if rc:
+            raise RuntimeError(f"variant {v}: rc {rc}")
+
+    out = {"workload": "BASELINE config 3: 64M CSR keys of 8-256 B", "variants": {}}
+    for v in args.variants:
+        h1.zero_()
+        run(v)
+        torch.cuda.synchronize()
+        ok = bench.verify_chunks(h1, 0, chunks)["ok"]
+        print(f"variant {v}: parity {'OK' if ok else 'MISMATCH'}", flush=True)
+        if not ok:
+            sys.exit(1)
+    t0 = time.perf_counter()
+    while (time.perf_counter() - t0) * 1e3 < args.warm_ms:
+        run(args.variants[0])
+        torch.cuda.synchronize()
+    times = {v: [] for v in args.variants}
+    for _ in range(args.reps):
+        for v in args.variants:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            run(v)
+            e0.record()
+            for _ in range(args.launches):
+                run(v)
+            e1.record()
+            torch.cuda.synchronize()
+            times[v].append(e0.elapsed_time(e1) / args.launches * 1e3)
+    for v in args.variants:
+        out["variants"][v] = {"median_us": statistics.median(times[v]), "min_us": min(times[v]), "all_us": times[v]}
+    if args.phases and 1 in args.variants:
+        clk.zero_()
+        run(1)
+        torch.cuda.synchronize()
+        out["phases"] = analyse(clk.cpu().numpy().view("uint32"), nblk)
+    print(json.dumps(out, indent=1), flush=True)
+    if args.phases:
+        Path(args.phases).parent.mkdir(parents=True, exist_ok=True)
+        Path(args.phases).write_text(json.dumps(out, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
