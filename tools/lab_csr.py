@@ -24,6 +24,8 @@ sys.path.insert(0, str(ROOT))
 import bench  # noqa: E402  (digest helpers)
 
 _p, _u64 = ctypes.c_void_p, ctypes.c_uint64
+PROBES = {13, 14, 15, 16}  # variants whose hashes are wrong by design (timing probes)
+CLOCKED = {1, 2, 11, 12, 13, 14, 15, 16}  # variants that write phase-clock records
 PHASES = ["setup_offsets", "dma_issue", "sort", "dma_wait", "walk", "stores"]
 
 
@@ -69,7 +71,10 @@ def analyse(clk, n_blocks):
     walk_ns = d[:, 4]
     cyc = (m1 - m0) & 0xFFFFFFFF
     ok = walk_ns > 0
+    life = T[:, 6] - T[:, 0]
+    res["life_ns_mean"] = float(life.mean())
     res["walk"] = {"ns_per_step_mean": float((walk_ns[ok] / np.maximum(smax[ok], 1)).mean()),
+                   "cycles_per_step_mean": float((cyc[ok] / np.maximum(smax[ok], 1)).mean()),
                    "clock_mhz_mean": float((cyc[ok] / walk_ns[ok] * 1e3).mean()),
                    "steps_max_mean": float(smax.mean()), "lane_fill": float(ssum.sum() / (64 * smax.sum()))}
     simd = (xcc << 16) | ((hw >> 4) & 0xFFF)  # xcc | se,sh,cu,simd bits of HW_ID
@@ -134,15 +139,18 @@ def main():
         run(v)
         torch.cuda.synchronize()
         ok = bench.verify_chunks(h1, 0, chunks)["ok"]
-        print(f"variant {v}: parity {'OK' if ok else 'MISMATCH'}", flush=True)
-        if not ok:
+        probe = v in PROBES
+        print(f"variant {v}: parity {'OK' if ok else 'MISMATCH'}{' (probe: wrong by design)' if probe else ''}",
+              flush=True)
+        if not ok and not probe:
             sys.exit(1)
     t0 = time.perf_counter()
     while (time.perf_counter() - t0) * 1e3 < args.warm_ms:
         run(args.variants[0])
         torch.cuda.synchronize()
     times = {v: [] for v in args.variants}
-    for _ in range(args.reps):
+    out["phases"] = {}
+    for rep in range(args.reps):
         for v in args.variants:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             run(v)
@@ -152,13 +160,13 @@ def main():
             e1.record()
             torch.cuda.synchronize()
             times[v].append(e0.elapsed_time(e1) / args.launches * 1e3)
+            if args.phases and v in CLOCKED and rep == args.reps - 1:
+                # the records of the batch's last launch: the same clock and thermal state
+                # as the timed launches (ADVICE: a lone launch after other variants is not)
+                out["phases"][v] = analyse(clk.cpu().numpy().view("uint32"), nblk)
+                out["phases"][v]["batch_us_per_launch"] = times[v][-1]
     for v in args.variants:
         out["variants"][v] = {"median_us": statistics.median(times[v]), "min_us": min(times[v]), "all_us": times[v]}
-    if args.phases and 1 in args.variants:
-        clk.zero_()
-        run(1)
-        torch.cuda.synchronize()
-        out["phases"] = analyse(clk.cpu().numpy().view("uint32"), nblk)
     print(json.dumps(out, indent=1), flush=True)
     if args.phases:
         Path(args.phases).parent.mkdir(parents=True, exist_ok=True)
