@@ -45,8 +45,9 @@ __device__ inline uint4 ld16(const uint8_t* p) {
   return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-__device__ inline void hash_cstr(const uint8_t* __restrict__ f, uint64_t off, uint64_t len, const SpadTable& sp,
-                                 uint64_t& h1, uint64_t& h2) {
+// The key [off, off + len) + NUL.  Callers go through hash_cstr_checked below, never this.
+__device__ inline void hash_cstr_unchecked(const uint8_t* __restrict__ f, uint64_t off, uint64_t len,
+                                           const SpadTable& sp, uint64_t& h1, uint64_t& h2) {
   uint64_t raw = sp.v[0];  // the seed
   if (len) {
     const uint64_t k = (len + 15) / 16;
@@ -89,6 +90,18 @@ __device__ inline void hash_cstr(const uint8_t* __restrict__ f, uint64_t off, ui
   h2 = len ? raw : h1;
 }
 
+// The only entry to the file hash: a key range outside the file -- impossible for
+// a correct scan state -- gives zero hashes (wrong records that parity catches), never a read
+// past the file.
+__device__ inline void hash_cstr_checked(const uint8_t* __restrict__ f, uint64_t size, uint64_t off, uint64_t len,
+                                         const SpadTable& sp, uint64_t& h1, uint64_t& h2) {
+  if (off <= size && len <= size - off) {
+    hash_cstr_unchecked(f, off, len, sp, h1, h2);
+  } else {
+    h1 = h2 = 0;
+  }
+}
+
 __global__ __launch_bounds__(kThreads) void import_hash_kernel(const uint8_t* __restrict__ f, uint64_t size,
                                                                const k2h_amd_import_rec* __restrict__ recs,
                                                                uint64_t n, SpadTable sp, uint64_t* __restrict__ h1,
@@ -96,8 +109,8 @@ __global__ __launch_bounds__(kThreads) void import_hash_kernel(const uint8_t* __
   const uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
   if (i >= n) return;
   const uint64_t off = recs[i].key_off, len = recs[i].key_len;
-  uint64_t a = 0, b = 0;
-  if (off <= size && len <= size - off) hash_cstr(f, off, len, sp, a, b);  // else: never read past the file
+  uint64_t a, b;
+  hash_cstr_checked(f, size, off, len, sp, a, b);
   __builtin_nontemporal_store(a, h1 + i);  // (consecutive lanes, consecutive i; never read back here)
   if (h2) __builtin_nontemporal_store(b, h2 + i);
 }
@@ -943,10 +956,8 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       if (hit) {
         a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
         c = e > s.fs ? raw : a;
-      } else if (s.fs <= e && e <= size) {
-        hash_cstr(f, s.fs, e - s.fs, sp, a, c);
       } else {  // a state outside the file (never for correct states): wrong records, not a fault
-        a = c = 0;
+        hash_cstr_checked(f, size, s.fs, e - s.fs, sp, a, c);
       }
       if (staged) {
         s_h[2 * x] = a;
@@ -1063,8 +1074,8 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     for (uint32_t x = threadIdx.x; x < nrec; x += 64)
       if (s_fh[x] == 2) {
         const uint64_t o = s_rec[4 * x], n = s_rec[4 * x + 1];
-        uint64_t a = 0, c = 0;
-        if (o <= size && n <= size - o) hash_cstr(f, o, n, sp, a, c);  // (else: a wrong state; wrong records, no fault)
+        uint64_t a, c;
+        hash_cstr_checked(f, size, o, n, sp, a, c);  // (a wrong state: wrong records, no fault)
         s_h[2 * x] = a;
         s_h[2 * x + 1] = c;
         s_fh[x] = 1;

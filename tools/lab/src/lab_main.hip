@@ -4,3 +4,5 @@
 #include "k2h_csr.hip"
 
 #include "lab_csr_clock.inc"
+#include "lab_csr_setup.inc"
+#include "lab_csr_entry.inc"

@@ -25,7 +25,7 @@ import bench  # noqa: E402  (digest helpers)
 
 _p, _u64 = ctypes.c_void_p, ctypes.c_uint64
 PROBES = {13, 14, 15, 16}  # variants whose hashes are wrong by design (timing probes)
-CLOCKED = {1, 2, 11, 12, 13, 14, 15, 16}  # variants that write phase-clock records
+CLOCKED = {1, 2, 3, 4, 5, 11, 12, 13, 14, 15, 16}  # variants that write phase-clock records
 PHASES = ["setup_offsets", "dma_issue", "sort", "dma_wait", "walk", "stores"]
 
 
