@@ -512,9 +512,25 @@ constexpr uint32_t kPre = 256;
 constexpr uint32_t kSpecLenMax = 254;  // longest key a slot holds (0xFF: no slot)
 // Each span's slots: the FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
 // at raw[kSlots * span + j], written only for the slots its packed word names.
+// Round 6: a unit's named slots are stored compacted, in span order (slot 0 before slot 1),
+// at the front of the unit's region raw[kUnitSlots * unit ..]; pass B finds a span's entry
+// from the named slots of the spans before it in its wave (slot_rank).
+constexpr uint32_t kUnitSlots = 64 * kSlots;
 struct SpecSlots {
-  uint64_t* raw;  // [nblk * kTThreads * kSlots]
+  uint64_t* raw;  // [nblk * kUnitsPerBlock * kUnitSlots]
 };
+// A lane's named slots and their rank among its wave's: entries p (slot 0, if v0) and
+// p + v0 (slot 1, if v1); n = the wave's total.
+struct SlotRank {
+  uint32_t v0, v1, p, n;
+};
+__device__ inline SlotRank slot_rank(bool v0, bool v1) {
+  const uint64_t b0 = __ballot(v0), b1 = __ballot(v1);
+  const uint32_t p0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u));
+  const uint32_t p1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
+  return SlotRank{v0 ? 1u : 0u, v1 ? 1u : 0u, p0 + p1,
+                  (uint32_t)__builtin_popcountll(b0) + (uint32_t)__builtin_popcountll(b1)};
+}
 
 // Newline state of a span for the speculative keys: whether it holds a newline, whether
 // the last one is still open (no cut after it), and its block-relative position; composed
@@ -769,20 +785,27 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
       slot[h] = k >> 24;
     }
   }
-  // The states go out as one 16-byte store per span (both slots; a slot no key took holds
-  // whatever the LDS held): through the staged block's LDS, free once every key is hashed.
-  // (Stored where they were hashed, 8 bytes at a time into the sparse slot array, they
-  // cost pass A +14 us: partial-line writes.)
+  // The states go out compacted per unit (round 6): each wave's (pass-B unit's) named slots
+  // in span order at the front of the unit's region of kUnitSlots entries, written as
+  // consecutive 8-byte pieces across the wave -- only the ~60 states a unit holds, not 16 B
+  // for each of its 64 spans (round 5: 1.34x the algorithmic bytes per call, a third of the
+  // excess these slots).  Through the staged block's LDS, free once every key is hashed.
   __syncthreads();
   uint64_t* s_raw = reinterpret_cast<uint64_t*>(lds);  // [kTThreads * kSlots]
 #pragma unroll
   for (uint32_t h = 0; h < 2; ++h)
     if (slot[h] != 0xFFFFFFFFu) s_raw[slot[h]] = raw[h];
   __syncthreads();
-  typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
-  static_assert(kSlots == 2, "one 16-byte store per span");
-  *reinterpret_cast<u64x2a*>(spec.raw + bid * (kTThreads * kSlots) + kSlots * threadIdx.x) =
-      *reinterpret_cast<const u64x2a*>(s_raw + kSlots * threadIdx.x);
+  const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+  const SlotRank sr = slot_rank(key0 != kNoKey, key1 != kNoKey);
+  uint64_t* s_comp = s_raw + kTThreads * kSlots + kUnitSlots * wv;  // [kUnitSlots] per wave
+  static_assert(8 * (kTThreads * kSlots + kUnitSlots * (kTThreads / 64)) <= kTChunk, "in the staged block's LDS");
+  if (sr.v0) s_comp[sr.p] = s_raw[kSlots * threadIdx.x];
+  if (sr.v1) s_comp[sr.p + sr.v0] = s_raw[kSlots * threadIdx.x + 1];
+  __syncthreads();
+  uint64_t* dst = spec.raw + (bid * kUnitsPerBlock + wv) * kUnitSlots;
+  if (ln < sr.n) dst[ln] = s_comp[ln];
+  if (ln + 64u < sr.n) dst[ln + 64u] = s_comp[ln + 64u];
 }
 
 // The entry-state scan between the passes, one block per tile: the tile's functions into
@@ -872,12 +895,15 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   const GFn ein = intile[blockIdx.x];
   const TState tin = tile_in[blk / kTile];
   const bool over = ev_count(pk) == 7u;
-  // the span's slots, loaded with its packed word (a slot pass A did not write holds a
-  // stale state, used only when the packed word names it)
-  static_assert(kSlots == 2, "one 16-byte load per span");
+  // The unit's compacted slot states (pass A): the first 64 loaded with the packed word, at
+  // a fixed address (no dependent round trip); a span takes its entries from the lanes that
+  // hold them once its packed word shows the named slots before it (a slot not named holds
+  // 0, used only when the packed word names it).
+  static_assert(kSlots == 2, "two slots per span");
   typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
   u64x2a sl_raw = u64x2a{0, 0};
-  if (HASH && !MDBM && live) sl_raw = *reinterpret_cast<const u64x2a*>(spec_raw + kSlots * ti);
+  uint64_t e_lo = 0;
+  if constexpr (HASH && !MDBM) e_lo = spec_raw[(uint64_t)kUnitSlots * blockIdx.x + threadIdx.x];
   // a span with more than kEvCap events (rare): its candidate masks from the file, each
   // candidate's byte read back (no LDS, so the kernel keeps its occupancy)
   uint64_t om0 = 0, om1 = 0;
@@ -900,6 +926,24 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       }
     }
     cand_masks(w, om0, om1);
+  }
+  if constexpr (HASH && !MDBM) {
+    const SlotRank sr = slot_rank(((pk >> 48) & 0xFFu) != 0xFFu, ((pk >> 56) & 0xFFu) != 0xFFu);
+    uint64_t e_hi = 0;
+    if (sr.n > 64u) e_hi = spec_raw[(uint64_t)kUnitSlots * blockIdx.x + 64u + threadIdx.x];  // wave-uniform, rare
+    auto pick = [&](uint32_t idx) -> uint64_t {  // entry idx of the unit, from the lane that loaded it
+      const int a = (int)((idx & 63u) << 2);
+      uint64_t v = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(e_lo >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)e_lo);
+      if (sr.n > 64u) {
+        const uint64_t w = ((uint64_t)(uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(e_hi >> 32)) << 32) |
+                           (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)e_hi);
+        v = idx < 64u ? v : w;
+      }
+      return v;
+    };
+    const uint64_t r0 = pick(sr.p), r1 = pick(sr.p + sr.v0);  // (all lanes: bpermute reads every lane)
+    sl_raw = u64x2a{sr.v0 ? r0 : 0ull, sr.v1 ? r1 : 0ull};
   }
   auto for_events = [&](auto&& fn) {
     if (!live) return;
@@ -1139,7 +1183,7 @@ static int launch_scan(const uint8_t* f, uint64_t size, k2h_amd_import_rec* recs
   const size_t nfn = nblk * kUnitsPerBlock;  // pass A writes every wave's function, past-EOF ones too
   const size_t o_fn = 0, o_in = o_fn + align256(nfn * sizeof(GFn)), o_tf = o_in + align256(nfn * sizeof(GFn));
   const size_t o_ti = o_tf + align256(ntile * sizeof(GFn)), o_ev = o_ti + align256(ntile * sizeof(TState));
-  const size_t nspec = MDBM ? 0 : nblk * kTThreads * kSlots;
+  const size_t nspec = MDBM ? 0 : nblk * kUnitsPerBlock * kUnitSlots;
   const size_t o_spec = o_ev + align256(nblk * kTThreads * 8);
   const size_t total = o_spec + align256(nspec * 8);
   ScanScratch& sc = g_scan[dev];
