@@ -202,76 +202,6 @@ __device__ __forceinline__ void fnv_step_last(uint32_t& lo, uint32_t& hi, uint32
                : K2H_P_CLOBBERS);
 }
 
-// ---------------------------------------------------------------------------
-// Split-chain chunk step (round 6).  The form above feeds t = x_hi*435 + (x_lo << 8) into
-// the mad64 that also produces the next lo, so the next byte's x_lo waits for the hi side:
-// four dependent ops per byte (mad64 -> xor hi -> mul_lo -> lshl_add -> mad64).  A wave
-// that is alone on its SIMD -- the CSR kernel's normal state: its two co-resident tiles
-// alternate between setup and walk -- runs that chain latency-bound at ~36 cycles per
-// byte against ~22.5 of issue (tools/lab_csr.py probes, profiles/r06c_csr_probes.json).
-// Here the two halves are separate chains of two ops each:
-//     {lo, c} = x_lo * 435                        v_mad_u64_u32 (addend 0)
-//     t'      = (x_lo << 8) + c                   v_lshl_add_u32
-//     hi      = lo32(x_hi * 435 + {t', 0})        v_mad_u64_u32 (odd half junk)
-// the same five ops per byte, and the hi chain runs one byte behind the lo chain, so in
-// each byte's issue order every operand was produced two or more slots earlier:
-//     xor lo(n) | mad hi(n-1) | mad lo(n) | xor hi(n) | lshl_add(n)
-// Register window: v48 lo / v49 c (pair), v50 t' / v51 = 0 (pair), v52 x_lo, v53 x_hi,
-// v62 hi / v63 junk (pair), v54 / v58 sign smears, v[56:57] shifted words, v[60:61] the
-// second-hash snapshot.  The state is (v48, v62).
-// ---------------------------------------------------------------------------
-#define K2H_Y_LOX(W, K)                                                                              \
-  "v_xor_b32_sdwa v52, sext(" W "), v48 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #K        \
-  " src1_sel:DWORD\n\t"
-#define K2H_Y_HIX(U, K)                                                                              \
-  "v_xor_b32_sdwa v53, sext(" U "), v62 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_" #K        \
-  " src1_sel:DWORD\n\t"
-#define K2H_Y_MAD1 "v_mad_u64_u32 v[48:49], vcc, v52, %[p], 0\n\t"
-#define K2H_Y_LSHL "v_lshl_add_u32 v50, v52, 8, v49\n\t"
-#define K2H_Y_MAD2 "v_mad_u64_u32 v[62:63], vcc, v53, %[p], v[50:51]\n\t"
-// byte K of word W (smear U): the chunk's first byte has no hi step of a previous byte
-#define K2H_Y_B0(W, U, K) K2H_Y_LOX(W, K) K2H_Y_MAD1 K2H_Y_HIX(U, K) K2H_Y_LSHL
-#define K2H_Y_BN(W, U, K) K2H_Y_LOX(W, K) K2H_Y_MAD2 K2H_Y_MAD1 K2H_Y_HIX(U, K) K2H_Y_LSHL
-#define K2H_Y_WORD(W, U) K2H_Y_BN(W, U, 0) K2H_Y_BN(W, U, 1) K2H_Y_BN(W, U, 2) K2H_Y_BN(W, U, 3)
-#define K2H_Y_WORD0(W, U) K2H_Y_B0(W, U, 0) K2H_Y_BN(W, U, 1) K2H_Y_BN(W, U, 2) K2H_Y_BN(W, U, 3)
-// the last word of a key: the snapshot (state after byte 14) between byte 15's hi step of
-// byte 14 and its own lo step
-#define K2H_Y_WORDL(W, U)                                                                            \
-  K2H_Y_BN(W, U, 0) K2H_Y_BN(W, U, 1) K2H_Y_BN(W, U, 2) K2H_Y_LOX(W, 3) K2H_Y_MAD2                   \
-  "v_mov_b32 v60, v48\n\tv_mov_b32 v61, v62\n\t" K2H_Y_MAD1 K2H_Y_HIX(U, 3) K2H_Y_LSHL
-#define K2H_Y_PAIR0(LO, HI, PAIR) K2H_X_SMEAR2(LO, HI, PAIR) K2H_Y_WORD0(LO, "v54") K2H_Y_WORD(HI, "v58")
-#define K2H_Y_PAIR(LO, HI, PAIR) K2H_X_SMEAR2(LO, HI, PAIR) K2H_Y_WORD(LO, "v54") K2H_Y_WORD(HI, "v58")
-#define K2H_Y_PAIRL(LO, HI, PAIR) K2H_X_SMEAR2(LO, HI, PAIR) K2H_Y_WORD(LO, "v54") K2H_Y_WORDL(HI, "v58")
-#define K2H_Y_CLOBBERS "v49", "v50", "v52", "v53", "v54", "v56", "v57", "v58", "v63", "vcc", "memory"
-
-// 16 bytes into the state (lo in v48, hi in v62); BANK as fnv_chunk16.
-template <int BANK = 0>
-__device__ __forceinline__ void fnv_chunk16y(uint32_t& lo, uint32_t& hi, uint4 c) {
-  if constexpr (BANK == 0) {
-    asm(K2H_Y_PAIR0("v40", "v41", "v[40:41]") K2H_Y_PAIR("v42", "v43", "v[42:43]") K2H_Y_MAD2
-        : "+{v48}"(lo), "+{v62}"(hi)
-        : "{v40}"(c.x), "{v41}"(c.y), "{v42}"(c.z), "{v43}"(c.w), "{v51}"(0u), [p] "s"(kPrimeLo),
-          [sel] "s"(kSmearSel)
-        : K2H_Y_CLOBBERS);
-  } else {
-    asm(K2H_Y_PAIR0("v44", "v45", "v[44:45]") K2H_Y_PAIR("v46", "v47", "v[46:47]") K2H_Y_MAD2
-        : "+{v48}"(lo), "+{v62}"(hi)
-        : "{v44}"(c.x), "{v45}"(c.y), "{v46}"(c.z), "{v47}"(c.w), "{v51}"(0u), [p] "s"(kPrimeLo),
-          [sel] "s"(kSmearSel)
-        : K2H_Y_CLOBBERS);
-  }
-}
-
-// The key's last chunk: also the state before its final byte (lo2, hi2).
-__device__ __forceinline__ void fnv_chunk16y_last(uint32_t& lo, uint32_t& hi, uint32_t& lo2, uint32_t& hi2,
-                                                  uint4 c) {
-  asm(K2H_Y_PAIR0("v40", "v41", "v[40:41]") K2H_Y_PAIRL("v42", "v43", "v[42:43]") K2H_Y_MAD2
-      : "+{v48}"(lo), "+{v62}"(hi), "={v60}"(lo2), "={v61}"(hi2)
-      : "{v40}"(c.x), "{v41}"(c.y), "{v42}"(c.z), "{v43}"(c.w), "{v51}"(0u), [p] "s"(kPrimeLo),
-        [sel] "s"(kSmearSel)
-      : K2H_Y_CLOBBERS);
-}
-
 // 32 bytes (two chunks), one statement.
 __device__ __forceinline__ void fnv_chunk32(uint32_t& lo, uint32_t& hi, uint4 a, uint4 b) {
   asm(K2H_P_PAIR("v40", "v41", "v[40:41]") K2H_P_PAIR("v42", "v43", "v[42:43]")

@@ -3,6 +3,8 @@
 // sources are in git history (tools/lab/README.md).
 #include "k2h_csr.hip"
 
+#include "lab_fnv_y.inc"
+
 #include "lab_csr_clock.inc"
 #include "lab_csr_setup.inc"
 #include "lab_csr_entry.inc"
