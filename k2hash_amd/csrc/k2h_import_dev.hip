@@ -631,7 +631,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   constexpr uint32_t PRE = MDBM ? 0u : kPre;
   __shared__ __attribute__((aligned(16))) uint8_t lds[16 + PRE + kTChunk];
   // The block's speculative keys in chunk-count order, one word each: start (16 bits,
-  // signed) | len << 16 | slot << 24, slot = span * kSlots + cut index.  A span's (at most
+  // signed) | len << 16 | entry << 24, entry = the key's place in its unit's compacted slot
+  // list (wave << 7 | rank, round 6; before: span * kSlots + cut index).  A span's (at most
   // kSlots) keys stay in its lane's registers until the sort (round 4; round 3: a list
   // filled by LDS atomics inside the event walk, each append a wave-wide wait for its
   // return).  (The block's LDS must stay within 17.5 KiB for 9 blocks per CU -- one
@@ -749,6 +750,12 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   // hash loop runs as long as ITS longest key: on BASELINE-like files (keys 8-64 B, 1-4
   // chunks) wave 0 takes the short keys and runs 2 chunks instead of 4 (round 4).
   static_assert(kSlots == 2 && kSpecLenMax < 256 && kTThreads * kSlots <= 256, "slot | len | start in 32 bits");
+  // each key's entry in its unit's compacted slot list (span order; see SpecSlots): wave
+  // bit 7, rank bits 0-6 -- carried in the sorted word instead of the raw slot index, so
+  // the hashing lane stores the state straight into its compacted place (round 6)
+  const SlotRank sr = slot_rank(key0 != kNoKey, key1 != kNoKey);
+  const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+  const uint32_t cidx[2] = {(wv << 7) | sr.p, (wv << 7) | (sr.p + sr.v0)};
   uint32_t cls[2];
   const uint32_t kk[2] = {key0, key1};
 #pragma unroll
@@ -770,7 +777,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   __syncthreads();
 #pragma unroll
   for (uint32_t h = 0; h < 2; ++h)
-    if (kk[h] != kNoKey) s_sorted[atomicAdd(&s_cls[cls[h]], 1u)] = kk[h] | ((kSlots * threadIdx.x + h) << 24);
+    if (kk[h] != kNoKey) s_sorted[atomicAdd(&s_cls[cls[h]], 1u)] = kk[h] | (cidx[h] << 24);
   __syncthreads();
   const uint32_t nk = s_cls[7];  // (each class's offset has moved to its end: the last is the count)
   uint64_t raw[2];
@@ -788,24 +795,18 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   // The states go out compacted per unit (round 6): each wave's (pass-B unit's) named slots
   // in span order at the front of the unit's region of kUnitSlots entries, written as
   // consecutive 8-byte pieces across the wave -- only the ~60 states a unit holds, not 16 B
-  // for each of its 64 spans (round 5: 1.34x the algorithmic bytes per call, a third of the
-  // excess these slots).  Through the staged block's LDS, free once every key is hashed.
+  // for each of its 64 spans (round 5: 1.34x the algorithmic bytes per call, over half of
+  // the excess these slots).  Through the staged block's LDS, free once every key is hashed.
   __syncthreads();
-  uint64_t* s_raw = reinterpret_cast<uint64_t*>(lds);  // [kTThreads * kSlots]
+  uint64_t* s_comp = reinterpret_cast<uint64_t*>(lds);  // [kTThreads / 64][kUnitSlots]
+  static_assert(kUnitSlots == 128 && kTThreads / 64 <= 2, "wave bit 7 | rank bits 0-6");
 #pragma unroll
   for (uint32_t h = 0; h < 2; ++h)
-    if (slot[h] != 0xFFFFFFFFu) s_raw[slot[h]] = raw[h];
-  __syncthreads();
-  const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
-  const SlotRank sr = slot_rank(key0 != kNoKey, key1 != kNoKey);
-  uint64_t* s_comp = s_raw + kTThreads * kSlots + kUnitSlots * wv;  // [kUnitSlots] per wave
-  static_assert(8 * (kTThreads * kSlots + kUnitSlots * (kTThreads / 64)) <= kTChunk, "in the staged block's LDS");
-  if (sr.v0) s_comp[sr.p] = s_raw[kSlots * threadIdx.x];
-  if (sr.v1) s_comp[sr.p + sr.v0] = s_raw[kSlots * threadIdx.x + 1];
+    if (slot[h] != 0xFFFFFFFFu) s_comp[slot[h]] = raw[h];
   __syncthreads();
   uint64_t* dst = spec.raw + (bid * kUnitsPerBlock + wv) * kUnitSlots;
-  if (ln < sr.n) dst[ln] = s_comp[ln];
-  if (ln + 64u < sr.n) dst[ln + 64u] = s_comp[ln + 64u];
+  if (ln < sr.n) dst[ln] = s_comp[kUnitSlots * wv + ln];
+  if (ln + 64u < sr.n) dst[ln + 64u] = s_comp[kUnitSlots * wv + ln + 64u];
 }
 
 // The entry-state scan between the passes, one block per tile: the tile's functions into
