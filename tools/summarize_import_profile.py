@@ -6,6 +6,9 @@ calls -> profiles/traffic_import.json, profiles/valu_import.json (bench.py's
 secondary.import roofline) and profiles/<tag>_import_summary.json.
 
     python tools/summarize_import_profile.py gpurun_out/prof_import r02ar
+    python tools/summarize_import_profile.py gpurun_out/prof_import_mdbm r06k import_mdbm
+(the mdbm form: tools/gpu/import_prof.sh with MDBM=1 -> profiles/traffic_import_mdbm.json,
+valu_import_mdbm.json, bench.py's secondary.import_mdbm roofline)
 """
 import collections
 import csv
@@ -25,6 +28,7 @@ def ours(name):
 
 def main():
     src, tag = Path(sys.argv[1]), sys.argv[2]
+    name = sys.argv[3] if len(sys.argv) > 3 else "import"
     prof = ROOT / "profiles"
     # kernel time per call from the trace: the last 10 calls' dispatches of our kernels
     rows = [r for r in csv.DictReader(open(src / "trace" / "run_kernel_trace.csv")) if ours(r["Kernel_Name"])]
@@ -37,7 +41,7 @@ def main():
         key = next((k for k in OURS[:4] if k in nm), "lookback_scan" if "lookback" in nm else "rocprim_scan")
         per[key] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / calls
     gpu_us = sum(per.values()) / 1e3
-    shutil.copy(src / "trace" / "run_kernel_stats.csv", prof / f"{tag}_import_kernel_stats.csv")
+    shutil.copy(src / "trace" / "run_kernel_stats.csv", prof / f"{tag}_{name}_kernel_stats.csv")
     # PMC: per counter, summed over our kernels, averaged over the calls of each pass
     pmc = {}
     for p in sorted(src.glob("pmc*")):
@@ -53,19 +57,20 @@ def main():
             pmc[k] = v / ncalls
     traffic = int(2 * pmc["FETCH_SIZE"] * 1024 + pmc["WRITE_SIZE"] * 1024)
     kern = " + ".join(sorted(per)) + " (one call)"
-    (prof / "traffic_import.json").write_text(json.dumps({
+    (prof / f"traffic_{name}.json").write_text(json.dumps({
         "kernel": kern, "hbm_bytes_per_launch": traffic, "FETCH_SIZE_kB": pmc["FETCH_SIZE"],
         "WRITE_SIZE_kB": pmc["WRITE_SIZE"], "formula": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
         "round": tag, "keys_per_launch": 1 << 23,
         "written_by": "tools/summarize_import_profile.py over tools/gpu/import_prof.sh"}, indent=1) + "\n")
-    (prof / "valu_import.json").write_text(json.dumps({
+    (prof / f"valu_{name}.json").write_text(json.dumps({
         "kernel": kern, "valu_insts_per_launch": pmc["SQ_INSTS_VALU"], "salu_insts_per_launch": pmc.get("SQ_INSTS_SALU"),
         "lds_insts_per_launch": pmc.get("SQ_INSTS_LDS"), "round": tag, "keys_per_launch": 1 << 23,
         "written_by": "tools/summarize_import_profile.py over tools/gpu/import_prof.sh"}, indent=1) + "\n")
     s = {"per_kernel_us_per_call": {k: v / 1e3 for k, v in per.items()}, "gpu_us_per_call": gpu_us,
          "pmc_per_call": pmc, "hbm_bytes_per_call": traffic,
-         "source": "tools/gpu/import_prof.sh: rocprofv3 over tools/import_step.py (8M-record TSV, 1.16 GB)"}
-    (prof / f"{tag}_import_summary.json").write_text(json.dumps(s, indent=1) + "\n")
+         "source": "tools/gpu/import_prof.sh: rocprofv3 over tools/import_step.py (8M records, 1.16 GB, "
+                   + ("mdbm" if name == "import_mdbm" else "TSV") + ")"}
+    (prof / f"{tag}_{name}_summary.json").write_text(json.dumps(s, indent=1) + "\n")
     print(json.dumps(s, indent=1))
 
 
