@@ -12,7 +12,7 @@ line's own algorithmic bytes per launch, beside the line's `roofline.frac`.  The
 entries time whole calls (three kernels and a host sync each), so their window is the
 range's span / steps and their per-call kernel sum is listed too.
 
-  python tools/summarize_line_profile.py <dir> <tag>   -> profiles/<tag>_line_summary.json
+  python tools/summarize_line_profile.py <dir> <tag> [out.json]   -> profiles/<tag>_line_summary.json
 """
 import csv
 import glob
@@ -76,7 +76,8 @@ def main():
         rec["frac_profile"] = algo / (rec["window_us"] * 1e-6) / HBM_PEAK
         rec["frac_profile_over_line"] = rec["frac_profile"] / rf["frac"]
         out["entries"][label] = rec
-    dst = Path(__file__).resolve().parents[1] / "profiles" / f"{tag}_line_summary.json"
+    dst = Path(sys.argv[3]) if len(sys.argv) > 3 else \
+        Path(__file__).resolve().parents[1] / "profiles" / f"{tag}_line_summary.json"
     dst.write_text(json.dumps(out, indent=1) + "\n")
     for k, v in out["entries"].items():
         print(f"{k:15s} window {v['window_us']:9.1f} us  frac profile {v['frac_profile']:.3f}  "
