@@ -313,6 +313,12 @@ def test_mdbm_digest_fixture_is_the_generators_file(oracle):
     sys.path.insert(0, str(GOLDEN))
     import make_import_digest as mk
 
+    sys.path.insert(0, str(GOLDEN.parents[1]))
+    import bench
+
+    assert bench.MDBM_HDR == mk.MDBM_HDR  # the device builder's header is the fixture's
+    assert (bench.IMPORT_KEY_LENS, bench.IMPORT_VAL_LENS, bench.IMPORT_BYTE_OFF) == (mk.KEY_LENS, mk.VAL_LENS,
+                                                                                      mk.BYTE_OFF)
     t = mk.build(2000)
     m = mk.build(2000, mdbm=True)
     h = len(mk.MDBM_HDR)
