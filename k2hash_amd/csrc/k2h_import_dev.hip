@@ -651,8 +651,11 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   const uint8_t* span = blk + 16 + rel;
   const bool live = base + rel < size;
   LFn acc = lfn_id();
-  uint64_t pk = kNoSlots;
-  uint32_t psh = 0, nl = 2u;  // psh: 9 x events so far; nl: no newline yet, and "no cut seen" (bit 1) until one is
+  // the span's events, newest at bits [36, 45) and the older ones moved down 9 bits each
+  // (round 6: one 64-bit shift per event instead of a variable shift and two guards); a span
+  // of ne <= kEvCap events holds them at [45 - 9 ne, 45) after the walk, shifted down then
+  uint64_t pk = 0;
+  uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
   // Speculative keys, found in the same walk (round 4; round 3 walked the packed events a
   // second time after the block scan): a cut that follows a newline of this span ends the
   // key that starts after it; the span's first cut, if no newline precedes it here, waits
@@ -661,38 +664,39 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   // state they met; the keys are assembled after it (round 5: a wave walks as many events
   // as its busiest lane, so per-event instructions cost 2.5x their mean share).
   uint32_t j = 0;                     // cut events so far
-  int32_t lnl = -1;                   // the last newline's position in the block while no cut followed it
-  uint32_t cp[kSlots] = {0, 0};       // cut h's position, h < kSlots
-  int32_t cl[kSlots] = {-1, -1};      // ... and lnl when it was read
-  uint32_t ns0 = 0;                   // a newline preceded cut 0 in the span
+  // cut h's position (bits 0-13) and the newline state it met (bits 14-29: nl before the
+  // cut; round 6: the last newline since the previous cut, and whether one preceded cut 0,
+  // read from it after the walk instead of being tracked per event)
+  uint32_t cw[kSlots] = {0, 0};
   constexpr uint32_t kNoKey = 0xFFFFFFFFu;
   uint32_t key0 = kNoKey, key1 = kNoKey;  // the span's keys at cuts 0 and 1: start | len << 16
   if (live)
     span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
       acc = lfn_push<MDBM>(acc, t, rel + o + 1);
       // (selects throughout: the branches hipcc made of these cost ~40 SALU per event)
-      const uint64_t e = (uint64_t)(o | (t << 7)) << (psh & 63u);
-      pk |= (t && psh < 9 * kEvCap) ? e : 0ull;
-      psh += t ? 9u : 0u;
-      const bool isnl = t == 1u;
-      const uint32_t nlv = 3u | ((rel + o) << 2), nlc = nl & (t ? ~2u : ~0u);
-      nl = isnl ? nlv : nlc;
+      pk = t ? (pk >> 9) | ((uint64_t)(o | (t << 7)) << 36) : pk;
+      ne += t ? 1u : 0u;
       if constexpr (!MDBM) {
         const bool cut = t >= 2u;  // TAB or NUL
-        const bool c0 = cut && j == 0, c1 = cut && j == 1;
-        cp[0] = c0 ? rel + o : cp[0];
-        cl[0] = c0 ? lnl : cl[0];
-        ns0 = c0 ? nl & 1u : ns0;
-        cp[1] = c1 ? rel + o : cp[1];
-        cl[1] = c1 ? lnl : cl[1];
-        lnl = cut ? -1 : isnl ? (int32_t)(rel + o) : lnl;
+        const uint32_t w = (rel + o) | (nl << 14);
+        cw[0] = (cut && j == 0) ? w : cw[0];
+        cw[1] = (cut && j == 1) ? w : cw[1];
         j += cut ? 1u : 0u;
       }
+      const uint32_t nlv = 3u | ((rel + o) << 2), nlc = nl & (t ? ~2u : ~0u);
+      nl = t == 1u ? nlv : nlc;
     });
+  const bool over = ne > kEvCap;
+  pk = (over ? 0ull : pk >> (9 * (kEvCap - ne))) | kNoSlots;
   uint32_t cut0 = 0xFFFFFFFFu;  // the span's first cut when no newline precedes it
   if constexpr (!MDBM) {
+    int32_t cl[kSlots];  // the last newline before cut h with no cut between them (-1: none)
+    uint32_t cp[kSlots];
 #pragma unroll
     for (uint32_t h = 0; h < kSlots; ++h) {
+      const uint32_t nlp = cw[h] >> 14;
+      cp[h] = cw[h] & 0x3FFFu;
+      cl[h] = (nlp & 3u) == 3u ? (int32_t)(nlp >> 2) : -1;
       const uint32_t len = cp[h] - (uint32_t)(cl[h] + 1);
       const bool em = j > h && cl[h] >= 0 && len <= kSpecLenMax;
       const uint32_t k = ((uint32_t)(cl[h] + 1) & 0xFFFFu) | (len << 16);
@@ -701,10 +705,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
       const uint64_t pkk = (pk & ~(0xFFull << (48 + 8 * h))) | ((uint64_t)(len & 0xFFu) << (48 + 8 * h));
       pk = em ? pkk : pk;
     }
-    cut0 = (j > 0 && cl[0] < 0 && !ns0) ? cp[0] : cut0;
+    cut0 = (j > 0 && cl[0] < 0) ? cp[0] : cut0;  // (cl[0] < 0: no newline before cut 0 in the span)
   }
-  const uint32_t ne = psh / 9u;
-  const bool over = ne > kEvCap;
   const LFn wf = wave_fn_reduce(s_wred[threadIdx.x >> 6], acc);
   if ((threadIdx.x & 63u) == 0) blk_fn[bid * kUnitsPerBlock + (threadIdx.x >> 6)] = gfn_of(wf, base);
   if constexpr (MDBM) {
