@@ -409,13 +409,14 @@ __device__ inline LFn lfn_push(const LFn& a, uint32_t t, uint32_t p1) {
 // word.  Pass B built it with one lfn_push per event, and a wave ran as many as its busiest
 // lane (4.7 per span against a mean of 1.9).  Entry bits: 0 / 1 exit mode entering in K /
 // V, [2, 4) / [4, 6) record ends, [6, 9) / [9, 12) boundary index (7: none), [12, 15) the
-// last NUL's index (7: none).
+// last NUL's index (7: none), [15, 18) (TSV) the index of the span's third cut event when the
+// event before it is a newline -- the key pass A hashes for its slot 2 (7: none).
 template <bool MDBM>
 struct SpanTab {
-  uint16_t v[1024];
+  uint32_t v[1024];
   constexpr SpanTab() : v() {
     for (uint32_t s = 0; s < 1024; ++s) {
-      uint32_t out = 0, nul = 7;
+      uint32_t out = 0, nul = 7, i2 = 7, ncut = 0, prev = 0;
       for (uint32_t m = 0; m < 2; ++m) {
         uint32_t mode = m, cnt = 0, last = 7;
         for (uint32_t i = 0; i < kEvCap; ++i) {
@@ -431,22 +432,32 @@ struct SpanTab {
         }
         out |= (mode << m) | (cnt << (2 + 2 * m)) | (last << (6 + 3 * m));
       }
-      for (uint32_t i = 0; i < kEvCap; ++i)
-        if (((s >> (2 * i)) & 3u) == 3u) nul = i;
-      v[s] = (uint16_t)(out | (nul << 12));
+      for (uint32_t i = 0; i < kEvCap; ++i) {
+        const uint32_t t = (s >> (2 * i)) & 3u;
+        if (t == 3u) nul = i;
+        if (!MDBM && t >= 2u) {
+          if (ncut == 2 && prev == 1u) i2 = i;
+          ++ncut;
+        }
+        prev = t;
+      }
+      v[s] = out | (nul << 12) | (i2 << 15);
     }
   }
 };
 __device__ const SpanTab<false> kSpanTabTsv{};
 __device__ const SpanTab<true> kSpanTabMdbm{};
 template <bool MDBM>
-__device__ inline LFn lfn_of_packed(uint64_t pk, uint32_t rel) {
+__device__ inline uint32_t span_tab(uint64_t pk) {
   static_assert(kEvCap == 5, "five 2-bit types index the table");
   const uint32_t lo = (uint32_t)pk, hi = (uint32_t)(pk >> 32);
   // types at bits 9 j + 7 of the word
   const uint32_t s = ((lo >> 7) & 3u) | ((lo >> 14) & 0xCu) | ((lo >> 21) & 0x30u) | ((hi << 4) & 0xC0u) |
                      ((hi >> 3) & 0x300u);
-  const uint32_t e = MDBM ? kSpanTabMdbm.v[s] : kSpanTabTsv.v[s];
+  return MDBM ? kSpanTabMdbm.v[s] : kSpanTabTsv.v[s];
+}
+template <bool MDBM>
+__device__ inline LFn lfn_of_packed(uint64_t pk, uint32_t rel, uint32_t e) {
   auto p1 = [&](uint32_t i) { return i < kEvCap ? rel + ((uint32_t)(pk >> (9 * i)) & 127u) + 1u : 0u; };
   return LFn{((e & 1u) ? kSelV : kSelK) | (((e & 2u) ? kSelV : kSelK) << 16), ((e >> 2) & 3u) | (((e >> 4) & 3u) << 16),
              p1((e >> 6) & 7u) | (p1((e >> 9) & 7u) << 16), p1((e >> 12) & 7u)};
@@ -519,17 +530,19 @@ constexpr uint32_t kUnitSlots = 64 * kSlots;
 struct SpecSlots {
   uint64_t* raw;  // [nblk * kUnitsPerBlock * kUnitSlots]
 };
-// A lane's named slots and their rank among its wave's: entries p (slot 0, if v0) and
-// p + v0 (slot 1, if v1); n = the wave's total.
+// A lane's named slots and their rank among its wave's: entries p (slot 0, if v0), p + v0
+// (slot 1, if v1) and p + v0 + v1 (slot 2, if v2); n = the wave's total.  Only entries below
+// kUnitSlots are stored (pass A) and taken (pass B); a key past them is hashed from the file.
 struct SlotRank {
-  uint32_t v0, v1, p, n;
+  uint32_t v0, v1, v2, p, n;
 };
-__device__ inline SlotRank slot_rank(bool v0, bool v1) {
-  const uint64_t b0 = __ballot(v0), b1 = __ballot(v1);
-  const uint32_t p0 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, 0u));
-  const uint32_t p1 = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, 0u));
-  return SlotRank{v0 ? 1u : 0u, v1 ? 1u : 0u, p0 + p1,
-                  (uint32_t)__builtin_popcountll(b0) + (uint32_t)__builtin_popcountll(b1)};
+__device__ inline uint32_t lanes_below(uint64_t b) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+__device__ inline SlotRank slot_rank(bool v0, bool v1, bool v2) {
+  const uint64_t b0 = __ballot(v0), b1 = __ballot(v1), b2 = __ballot(v2);
+  return SlotRank{v0 ? 1u : 0u, v1 ? 1u : 0u, v2 ? 1u : 0u, lanes_below(b0) + lanes_below(b1) + lanes_below(b2),
+                  (uint32_t)(__builtin_popcountll(b0) + __builtin_popcountll(b1) + __builtin_popcountll(b2))};
 }
 
 // Newline state of a span for the speculative keys: whether it holds a newline, whether
@@ -667,9 +680,9 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   // cut h's position (bits 0-13) and the newline state it met (bits 14-29: nl before the
   // cut; round 6: the last newline since the previous cut, and whether one preceded cut 0,
   // read from it after the walk instead of being tracked per event)
-  uint32_t cw[kSlots] = {0, 0};
+  uint32_t cw[3] = {0, 0, 0};  // (cut 2: the in-span key pass A hashes for slot 2, round 6)
   constexpr uint32_t kNoKey = 0xFFFFFFFFu;
-  uint32_t key0 = kNoKey, key1 = kNoKey;  // the span's keys at cuts 0 and 1: start | len << 16
+  uint32_t key0 = kNoKey, key1 = kNoKey, key2 = kNoKey;  // the span's keys at cuts 0-2: start | len << 16
   if (live)
     span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
       acc = lfn_push<MDBM>(acc, t, rel + o + 1);
@@ -681,6 +694,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
         const uint32_t w = (rel + o) | (nl << 14);
         cw[0] = (cut && j == 0) ? w : cw[0];
         cw[1] = (cut && j == 1) ? w : cw[1];
+        cw[2] = (cut && j == 2) ? w : cw[2];
         j += cut ? 1u : 0u;
       }
       const uint32_t nlv = 3u | ((rel + o) << 2), nlc = nl & (t ? ~2u : ~0u);
@@ -690,16 +704,20 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   pk = (over ? 0ull : pk >> (9 * (kEvCap - ne))) | kNoSlots;
   uint32_t cut0 = 0xFFFFFFFFu;  // the span's first cut when no newline precedes it
   if constexpr (!MDBM) {
-    int32_t cl[kSlots];  // the last newline before cut h with no cut between them (-1: none)
-    uint32_t cp[kSlots];
+    int32_t cl[3];  // the last newline before cut h with no cut between them (-1: none)
+    uint32_t cp[3];
 #pragma unroll
-    for (uint32_t h = 0; h < kSlots; ++h) {
+    for (uint32_t h = 0; h < 3; ++h) {
       const uint32_t nlp = cw[h] >> 14;
       cp[h] = cw[h] & 0x3FFFu;
       cl[h] = (nlp & 3u) == 3u ? (int32_t)(nlp >> 2) : -1;
       const uint32_t len = cp[h] - (uint32_t)(cl[h] + 1);
       const bool em = j > h && cl[h] >= 0 && len <= kSpecLenMax;
       const uint32_t k = ((uint32_t)(cl[h] + 1) & 0xFFFFu) | (len << 16);
+      if (h == 2) {  // no length byte: pass B finds it from the packed events (SpanTab), so not for a span past kEvCap
+        key2 = (em && !over) ? k : kNoKey;
+        continue;
+      }
       if (h == 0) key0 = em ? k : kNoKey;
       else key1 = em ? k : kNoKey;
       const uint64_t pkk = (pk & ~(0xFFull << (48 + 8 * h))) | ((uint64_t)(len & 0xFFu) << (48 + 8 * h));
@@ -751,17 +769,18 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   // The keys in order of chunk count (counting sort over 8 classes), so that each wave's
   // hash loop runs as long as ITS longest key: on BASELINE-like files (keys 8-64 B, 1-4
   // chunks) wave 0 takes the short keys and runs 2 chunks instead of 4 (round 4).
-  static_assert(kSlots == 2 && kSpecLenMax < 256 && kTThreads * kSlots <= 256, "slot | len | start in 32 bits");
+  static_assert(kSpecLenMax < 256 && kUnitSlots * (kTThreads / 64) <= 256, "slot | len | start in 32 bits");
   // each key's entry in its unit's compacted slot list (span order; see SpecSlots): wave
   // bit 7, rank bits 0-6 -- carried in the sorted word instead of the raw slot index, so
-  // the hashing lane stores the state straight into its compacted place (round 6)
-  const SlotRank sr = slot_rank(key0 != kNoKey, key1 != kNoKey);
+  // the hashing lane stores the state straight into its compacted place (round 6); a wave's
+  // entries past kUnitSlots are not hashed (pass B ranks the same way)
+  const SlotRank sr = slot_rank(key0 != kNoKey, key1 != kNoKey, key2 != kNoKey);
   const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
-  const uint32_t cidx[2] = {(wv << 7) | sr.p, (wv << 7) | (sr.p + sr.v0)};
-  uint32_t cls[2];
-  const uint32_t kk[2] = {key0, key1};
+  const uint32_t rk[3] = {sr.p, sr.p + sr.v0, sr.p + sr.v0 + sr.v1};
+  uint32_t cls[3], kk[3] = {key0, key1, key2};
 #pragma unroll
-  for (uint32_t h = 0; h < 2; ++h) {
+  for (uint32_t h = 0; h < 3; ++h) {
+    kk[h] = rk[h] < kUnitSlots ? kk[h] : kNoKey;
     cls[h] = min((kk[h] >> 16) + 15u, 128u) / 16u;  // 0..8
     cls[h] = cls[h] ? cls[h] - 1u : 0u;
     if (kk[h] != kNoKey) atomicAdd(&s_cls[cls[h]], 1u);
@@ -778,8 +797,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t h = 0; h < 2; ++h)
-    if (kk[h] != kNoKey) s_sorted[atomicAdd(&s_cls[cls[h]], 1u)] = kk[h] | (cidx[h] << 24);
+  for (uint32_t h = 0; h < 3; ++h)
+    if (kk[h] != kNoKey) s_sorted[atomicAdd(&s_cls[cls[h]], 1u)] = kk[h] | (((wv << 7) | rk[h]) << 24);
   __syncthreads();
   const uint32_t nk = s_cls[7];  // (each class's offset has moved to its end: the last is the count)
   uint64_t raw[2];
@@ -807,8 +826,9 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     if (slot[h] != 0xFFFFFFFFu) s_comp[slot[h]] = raw[h];
   __syncthreads();
   uint64_t* dst = spec.raw + (bid * kUnitsPerBlock + wv) * kUnitSlots;
-  if (ln < sr.n) dst[ln] = s_comp[kUnitSlots * wv + ln];
-  if (ln + 64u < sr.n) dst[ln + 64u] = s_comp[kUnitSlots * wv + ln + 64u];
+  const uint32_t nst = min(sr.n, kUnitSlots);
+  if (ln < nst) dst[ln] = s_comp[kUnitSlots * wv + ln];
+  if (ln + 64u < nst) dst[ln + 64u] = s_comp[kUnitSlots * wv + ln + 64u];
 }
 
 // The entry-state scan between the passes, one block per tile: the tile's functions into
@@ -902,9 +922,12 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   // a fixed address (no dependent round trip); a span takes its entries from the lanes that
   // hold them once its packed word shows the named slots before it (a slot not named holds
   // 0, used only when the packed word names it).
-  static_assert(kSlots == 2, "two slots per span");
-  typedef uint64_t u64x2a __attribute__((ext_vector_type(2)));
-  u64x2a sl_raw = u64x2a{0, 0};
+  // a span's slots: their states and the key length each holds, 8 bits per slot (0xFF:
+  // none; slots 0-1 from the packed word, slot 2 -- the third cut's key, when a newline is
+  // the event before it -- found from the packed events, round 6)
+  const uint32_t te = span_tab<MDBM>(pk);
+  uint64_t sl0 = 0, sl1 = 0, sl2 = 0;
+  uint32_t slen = 0xFFFFFFu;
   uint64_t e_lo = 0;
   if constexpr (HASH && !MDBM) e_lo = spec_raw[(uint64_t)kUnitSlots * blockIdx.x + threadIdx.x];
   // a span with more than kEvCap events (rare): its candidate masks from the file, each
@@ -931,7 +954,10 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     cand_masks(w, om0, om1);
   }
   if constexpr (HASH && !MDBM) {
-    const SlotRank sr = slot_rank(((pk >> 48) & 0xFFu) != 0xFFu, ((pk >> 56) & 0xFFu) != 0xFFu);
+    const uint32_t b0 = (uint32_t)(pk >> 48) & 0xFFu, b1 = (uint32_t)(pk >> 56) & 0xFFu, i2 = (te >> 15) & 7u;
+    const bool v2 = i2 < kEvCap;  // (then 2 <= i2: the event before it is the newline)
+    const uint32_t b2 = v2 ? ((uint32_t)(pk >> (9 * i2)) & 127u) - ((uint32_t)(pk >> (9 * i2 - 9)) & 127u) - 1u : 0xFFu;
+    const SlotRank sr = slot_rank(b0 != 0xFFu, b1 != 0xFFu, v2);
     uint64_t e_hi = 0;
     if (sr.n > 64u) e_hi = spec_raw[(uint64_t)kUnitSlots * blockIdx.x + 64u + threadIdx.x];  // wave-uniform, rare
     auto pick = [&](uint32_t idx) -> uint64_t {  // entry idx of the unit, from the lane that loaded it
@@ -945,8 +971,12 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       }
       return v;
     };
-    const uint64_t r0 = pick(sr.p), r1 = pick(sr.p + sr.v0);  // (all lanes: bpermute reads every lane)
-    sl_raw = u64x2a{sr.v0 ? r0 : 0ull, sr.v1 ? r1 : 0ull};
+    const uint32_t p1 = sr.p + sr.v0, p2 = p1 + sr.v1;
+    sl0 = pick(sr.p);  // (all lanes: bpermute reads every lane)
+    sl1 = pick(p1);
+    sl2 = pick(p2);
+    slen = (sr.p < kUnitSlots ? b0 : 0xFFu) | ((p1 < kUnitSlots ? b1 : 0xFFu) << 8) |
+           ((p2 < kUnitSlots ? b2 : 0xFFu) << 16);
   }
   auto for_events = [&](auto&& fn) {
     if (!live) return;
@@ -964,7 +994,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       }
     }
   };
-  LFn acc = lfn_of_packed<MDBM>(pk, rel);  // (a span past the file: no events, the identity)
+  LFn acc = lfn_of_packed<MDBM>(pk, rel, te);  // (a span past the file: no events, the identity)
   if (over) {  // more than kEvCap events (rare): from the file
     acc = lfn_id();
     for_events([&](uint32_t o, uint32_t t) { acc = lfn_push<MDBM>(acc, t, rel + o + 1); });
@@ -981,7 +1011,10 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     for (uint32_t q = threadIdx.x; q < nrec; q += 64) s_fk[q] = s_fv[q] = s_fh[q] = 0;
   __syncthreads();
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
-  uint32_t j = 0;           // cut events of this span so far
+  // the slot of this span's next cut event in sl0 and the low byte of slen: both move on at
+  // each cut (a select over three states by a cut counter made hipcc put the walk's
+  // captures in scratch)
+  slen |= 0xFF000000u;
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));  // recs: 8-byte aligned
   auto key_end = [&](uint64_t e) {
     if (s.r < HDR || s.r >= lim) return;
@@ -998,8 +1031,9 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       uint64_t a, c;
       // pass A's key for this cut event, if its length is this key's (0xFF: none)
       const uint64_t len = e - s.fs;
-      const bool hit = j < kSlots && len <= kSpecLenMax && ((pk >> (48 + 8 * j)) & 0xFFu) == len;
-      const uint64_t raw = j == 0 ? sl_raw.x : sl_raw.y;
+      const uint32_t sj = slen & 0xFFu;
+      const bool hit = sj != 0xFFu && len == sj;
+      const uint64_t raw = sl0;
       if (hit) {
         a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
         c = e > s.fs ? raw : a;
@@ -1064,8 +1098,9 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
         if (fe && s.m && s.r == 2) val_end(pos, nul);  // the fifth header line's check (record 2 < HDR)
       if constexpr (HASH) {
         const uint64_t len = pos - s.fs;
-        const bool hit = j < kSlots && len <= kSpecLenMax && ((pk >> (48 + 8 * j)) & 0xFFu) == len;
-        const uint64_t raw = j == 0 ? sl_raw.x : sl_raw.y;
+        const uint32_t sj = slen & 0xFFu;
+        const bool hit = sj != 0xFFu && len == sj;
+        const uint64_t raw = sl0;
         uint64_t a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
         uint64_t c = pos > s.fs ? raw : a;
         *reinterpret_cast<u64x2a16*>(&s_h[2 * xk]) = u64x2a16{a, c};
@@ -1081,7 +1116,11 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     s.fs = brk ? pos + 1 : s.fs;
     nulf = !brk && (nulf || nul);
     s.m = brk ? s.m ^ 1u : s.m;
-    j += nl ? 0u : 1u;  // cut events: TAB and NUL
+    if constexpr (HASH && !MDBM) {  // cut events: TAB and NUL
+      sl0 = nl ? sl0 : sl1;
+      sl1 = nl ? sl1 : sl2;
+      slen = nl ? slen : (slen >> 8) | 0xFF000000u;
+    }
   });
   if (live && base + rel + kTBytes >= size) {  // the thread holding the last byte
     if (s.m && !nulf) val_end(size, false);    // a value read to EOF
