@@ -347,13 +347,14 @@ __device__ inline uint32_t next_event(uint64_t& m0, uint64_t& m1) {
 
 // Events of a thread's span: NL / TAB / NUL bytes (types 1 / 2 / 3) in byte order.  Pass A
 // packs up to kEvCap of them into one word per thread for pass B: entry j = offset (7 bits)
-// | type << 7 at bits [9j, 9j + 9), the count at bits [45, 48) (7 = more than kEvCap: pass B
-// reads the span back from the file), and the lengths of the keys pass A hashed for the
-// span's first two cut events at bits [48, 56) and [56, 64) (0xFF: none; see kSlots).
-constexpr uint32_t kEvCap = 5;
-constexpr uint64_t kNoSlots = 0xFFFFull << 48;
-constexpr uint64_t kEvOverflow = (7ull << 45) | kNoSlots;
-__device__ inline uint32_t ev_count(uint64_t pk) { return (uint32_t)(pk >> 45) & 7u; }
+// | type << 7 at bits [9j, 9j + 9) (unused entries 0), bit 54 set for a span with more
+// (pass B reads it back from the file; the entries are then empty), and at bits [55, 63)
+// the length of the head key pass A hashed for the span's first cut (0xFF: none; see
+// kSlots).  Round 6: six entries, not five and a count -- the keys pass A hashes after an
+// in-span newline need no length byte (pass B finds them from the entries).
+constexpr uint32_t kEvCap = 6;
+constexpr uint64_t kEvOver = 1ull << 54;
+constexpr uint64_t kHeadNone = 0xFFull << 55;
 // 0x0A -> 1, 0x09 -> 2 (TSV only: a TAB is an ordinary byte of an mdbm line), 0x00 -> 3,
 // other bytes 0: two bits per byte value below 11
 template <bool MDBM>
@@ -403,20 +404,21 @@ __device__ inline LFn lfn_push(const LFn& a, uint32_t t, uint32_t p1) {
 }
 
 // The function of a span's packed events (at most kEvCap, pass A's word) by table (round 5):
-// it depends on their types and offsets only, so a 1024-entry table indexed by the five
+// it depends on their types and offsets only, so a 4096-entry table indexed by the six
 // 2-bit types (0: none) gives, per entry mode, the exit mode, the record ends and the index
 // of the last field boundary, plus the index of the last NUL; the offsets come from the
 // word.  Pass B built it with one lfn_push per event, and a wave ran as many as its busiest
 // lane (4.7 per span against a mean of 1.9).  Entry bits: 0 / 1 exit mode entering in K /
 // V, [2, 4) / [4, 6) record ends, [6, 9) / [9, 12) boundary index (7: none), [12, 15) the
-// last NUL's index (7: none), [15, 18) (TSV) the index of the span's third cut event when the
-// event before it is a newline -- the key pass A hashes for its slot 2 (7: none).
+// last NUL's index (7: none); TSV, round 6: [15, 18), [18, 21), [21, 24) the index of the
+// span's cut 0, 1, 2 when the event before it is a newline -- the in-span keys pass A
+// hashes for slots 0-2 (7: none); [24, 27) the number of events.
 template <bool MDBM>
 struct SpanTab {
-  uint32_t v[1024];
+  uint32_t v[4096];
   constexpr SpanTab() : v() {
-    for (uint32_t s = 0; s < 1024; ++s) {
-      uint32_t out = 0, nul = 7, i2 = 7, ncut = 0, prev = 0;
+    for (uint32_t s = 0; s < 4096; ++s) {
+      uint32_t out = 0, nul = 7, ins[3] = {7, 7, 7}, ncut = 0, prev = 0, ne = 0;
       for (uint32_t m = 0; m < 2; ++m) {
         uint32_t mode = m, cnt = 0, last = 7;
         for (uint32_t i = 0; i < kEvCap; ++i) {
@@ -436,12 +438,13 @@ struct SpanTab {
         const uint32_t t = (s >> (2 * i)) & 3u;
         if (t == 3u) nul = i;
         if (!MDBM && t >= 2u) {
-          if (ncut == 2 && prev == 1u) i2 = i;
+          if (ncut < 3 && prev == 1u) ins[ncut] = i;
           ++ncut;
         }
+        ne += t ? 1u : 0u;
         prev = t;
       }
-      v[s] = out | (nul << 12) | (i2 << 15);
+      v[s] = out | (nul << 12) | (ins[0] << 15) | (ins[1] << 18) | (ins[2] << 21) | (ne << 24);
     }
   }
 };
@@ -449,11 +452,11 @@ __device__ const SpanTab<false> kSpanTabTsv{};
 __device__ const SpanTab<true> kSpanTabMdbm{};
 template <bool MDBM>
 __device__ inline uint32_t span_tab(uint64_t pk) {
-  static_assert(kEvCap == 5, "five 2-bit types index the table");
+  static_assert(kEvCap == 6, "six 2-bit types index the table");
   const uint32_t lo = (uint32_t)pk, hi = (uint32_t)(pk >> 32);
   // types at bits 9 j + 7 of the word
   const uint32_t s = ((lo >> 7) & 3u) | ((lo >> 14) & 0xCu) | ((lo >> 21) & 0x30u) | ((hi << 4) & 0xC0u) |
-                     ((hi >> 3) & 0x300u);
+                     ((hi >> 3) & 0x300u) | ((hi >> 10) & 0xC00u);
   return MDBM ? kSpanTabMdbm.v[s] : kSpanTabTsv.v[s];
 }
 template <bool MDBM>
@@ -500,18 +503,19 @@ __device__ inline uint64_t key_raw_lds(const uint8_t* lds_key, uint32_t len, con
 
 // Speculative keys: pass A does not know the mode at its block's start, but a key starts
 // exactly after every newline the value getline reads, and ends at the first TAB or NUL
-// after it (the key getline's TAB, or the C-string cut).  So for every cut event (TAB /
-// NUL) that is the first after a newline of the same block, pass A hashes the bytes
-// between them: the j-th cut event of a span (j < kSlots) keeps the key's length in its
-// packed word and the raw state in the span's slot j (SpecSlots).  Pass B, whose walk ends
-// a key at cut event j of its span, takes the slot when the key's true length equals the
-// stored one (same end, same length: the same bytes); every other key (the file's first,
-// a key whose newline is in an earlier block, a third cut in one span, a span with more
-// than kEvCap events, a key of 255 bytes or more) is hashed from the file.
+// after it (the key getline's TAB, or the C-string cut).  So for the span's first three cut
+// events (TAB / NUL) that follow a newline of the same span, pass A hashes the bytes between
+// them (round 6: three, not two; such a key needs no length byte -- pass B finds it from
+// the packed events, the newline just before the cut), plus the head key below, whose
+// length rides in the packed word.  Pass B, whose walk ends a key at cut event c of its
+// span, takes slot c when the key's true length equals the slot's (same end, same length:
+// the same bytes); every other key (one whose newline is in an earlier block beyond the
+// head key's reach, a fourth cut in one span, a span with more than kEvCap events, a key of
+// 255 bytes or more, a wave's slots past kUnitSlots) is hashed from the file.
 // Round 4: slots indexed by span, so pass B loads its states with its packed word instead
 // of after it (round 3: a per-block list indexed from the packed word, 10 B per key -- a
 // second dependent HBM round trip at the start of every pass-B wave).
-constexpr uint32_t kSlots = 2;
+constexpr uint32_t kSlots = 2;  // slot states per span on average that a unit's region holds
 // The head key: the key that ends at a block's first cut event when no newline precedes it
 // in the block started in the bytes before the block (a key straddling the boundary, ~1 in
 // 4 blocks on BASELINE-like files).  Pass A stages kPre bytes before the block too and
@@ -664,9 +668,9 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   const uint8_t* span = blk + 16 + rel;
   const bool live = base + rel < size;
   LFn acc = lfn_id();
-  // the span's events, newest at bits [36, 45) and the older ones moved down 9 bits each
+  // the span's events, newest at bits [45, 54) and the older ones moved down 9 bits each
   // (round 6: one 64-bit shift per event instead of a variable shift and two guards); a span
-  // of ne <= kEvCap events holds them at [45 - 9 ne, 45) after the walk, shifted down then
+  // of ne <= kEvCap events holds them at [54 - 9 ne, 54) after the walk, shifted down then
   uint64_t pk = 0;
   uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
   // Speculative keys, found in the same walk (round 4; round 3 walked the packed events a
@@ -687,7 +691,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
       acc = lfn_push<MDBM>(acc, t, rel + o + 1);
       // (selects throughout: the branches hipcc made of these cost ~40 SALU per event)
-      pk = t ? (pk >> 9) | ((uint64_t)(o | (t << 7)) << 36) : pk;
+      pk = t ? (pk >> 9) | ((uint64_t)(o | (t << 7)) << 45) : pk;
       ne += t ? 1u : 0u;
       if constexpr (!MDBM) {
         const bool cut = t >= 2u;  // TAB or NUL
@@ -701,7 +705,8 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
       nl = t == 1u ? nlv : nlc;
     });
   const bool over = ne > kEvCap;
-  pk = (over ? 0ull : pk >> (9 * (kEvCap - ne))) | kNoSlots;
+  pk = over ? kEvOver : pk >> (9 * (kEvCap - ne));
+  uint32_t head_len = 0xFFu;  // the head key's length byte
   uint32_t cut0 = 0xFFFFFFFFu;  // the span's first cut when no newline precedes it
   if constexpr (!MDBM) {
     int32_t cl[3];  // the last newline before cut h with no cut between them (-1: none)
@@ -712,23 +717,20 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
       cp[h] = cw[h] & 0x3FFFu;
       cl[h] = (nlp & 3u) == 3u ? (int32_t)(nlp >> 2) : -1;
       const uint32_t len = cp[h] - (uint32_t)(cl[h] + 1);
-      const bool em = j > h && cl[h] >= 0 && len <= kSpecLenMax;
+      // (no length byte: pass B finds these keys from the packed events, so none for a span
+      // past kEvCap; in-span, len < 128)
+      const bool em = j > h && cl[h] >= 0 && !over;
       const uint32_t k = ((uint32_t)(cl[h] + 1) & 0xFFFFu) | (len << 16);
-      if (h == 2) {  // no length byte: pass B finds it from the packed events (SpanTab), so not for a span past kEvCap
-        key2 = (em && !over) ? k : kNoKey;
-        continue;
-      }
       if (h == 0) key0 = em ? k : kNoKey;
-      else key1 = em ? k : kNoKey;
-      const uint64_t pkk = (pk & ~(0xFFull << (48 + 8 * h))) | ((uint64_t)(len & 0xFFu) << (48 + 8 * h));
-      pk = em ? pkk : pk;
+      else if (h == 1) key1 = em ? k : kNoKey;
+      else key2 = em ? k : kNoKey;
     }
     cut0 = (j > 0 && cl[0] < 0) ? cp[0] : cut0;  // (cl[0] < 0: no newline before cut 0 in the span)
   }
   const LFn wf = wave_fn_reduce(s_wred[threadIdx.x >> 6], acc);
   if ((threadIdx.x & 63u) == 0) blk_fn[bid * kUnitsPerBlock + (threadIdx.x >> 6)] = gfn_of(wf, base);
   if constexpr (MDBM) {
-    ev[base / kTBytes + threadIdx.x] = over ? kEvOverflow : pk | ((uint64_t)ne << 45);
+    ev[base / kTBytes + threadIdx.x] = pk | kHeadNone;
     return;
   }
   uint32_t pre_nl;
@@ -759,13 +761,11 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     const uint32_t len = (uint32_t)((int32_t)cut0 - start);
     if (ok && len <= kSpecLenMax) {
       key0 = ((uint32_t)start & 0xFFFFu) | (len << 16);
-      pk = (pk & ~(0xFFull << 48)) | ((uint64_t)len << 48);
+      head_len = len;
     }
   }
-  // a span with more than kEvCap events keeps its slots: pass B re-reads its events from
-  // the file and counts its cuts the same way
-  pk = over ? (kEvOverflow & ~kNoSlots) | (pk & kNoSlots) : pk | ((uint64_t)ne << 45);
-  ev[base / kTBytes + threadIdx.x] = pk;
+  // (a span with more than kEvCap events keeps its head key: pass B reads its length byte)
+  ev[base / kTBytes + threadIdx.x] = pk | ((uint64_t)head_len << 55);
   // The keys in order of chunk count (counting sort over 8 classes), so that each wave's
   // hash loop runs as long as ITS longest key: on BASELINE-like files (keys 8-64 B, 1-4
   // chunks) wave 0 takes the short keys and runs 2 chunks instead of 4 (round 4).
@@ -917,7 +917,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   const uint64_t pk = ev[ti];
   const GFn ein = intile[blockIdx.x];
   const TState tin = tile_in[blk / kTile];
-  const bool over = ev_count(pk) == 7u;
+  const bool over = (pk & kEvOver) != 0;
   // The unit's compacted slot states (pass A): the first 64 loaded with the packed word, at
   // a fixed address (no dependent round trip); a span takes its entries from the lanes that
   // hold them once its packed word shows the named slots before it (a slot not named holds
@@ -954,10 +954,15 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     cand_masks(w, om0, om1);
   }
   if constexpr (HASH && !MDBM) {
-    const uint32_t b0 = (uint32_t)(pk >> 48) & 0xFFu, b1 = (uint32_t)(pk >> 56) & 0xFFu, i2 = (te >> 15) & 7u;
-    const bool v2 = i2 < kEvCap;  // (then 2 <= i2: the event before it is the newline)
-    const uint32_t b2 = v2 ? ((uint32_t)(pk >> (9 * i2)) & 127u) - ((uint32_t)(pk >> (9 * i2 - 9)) & 127u) - 1u : 0xFFu;
-    const SlotRank sr = slot_rank(b0 != 0xFFu, b1 != 0xFFu, v2);
+    // slot c: the key at cut c that starts after the newline just before it (event index
+    // i_c from the table; its length from the two offsets), or slot 0's head key (its byte)
+    auto inspan = [&](uint32_t i) {
+      return i < kEvCap ? ((uint32_t)(pk >> (9 * i)) & 127u) - ((uint32_t)(pk >> (9 * i - 9)) & 127u) - 1u : 0xFFu;
+    };
+    const uint32_t hb = (uint32_t)(pk >> 55) & 0xFFu;
+    const uint32_t b0 = hb != 0xFFu ? hb : inspan((te >> 15) & 7u), b1 = inspan((te >> 18) & 7u),
+                   b2 = inspan((te >> 21) & 7u);
+    const SlotRank sr = slot_rank(b0 != 0xFFu, b1 != 0xFFu, b2 != 0xFFu);
     uint64_t e_hi = 0;
     if (sr.n > 64u) e_hi = spec_raw[(uint64_t)kUnitSlots * blockIdx.x + 64u + threadIdx.x];  // wave-uniform, rare
     auto pick = [&](uint32_t idx) -> uint64_t {  // entry idx of the unit, from the lane that loaded it
@@ -987,7 +992,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
         if (t) fn(o, t);
       }
     } else {
-      const uint32_t ne = ev_count(pk);
+      const uint32_t ne = (te >> 24) & 7u;
       for (uint32_t j = 0; j < ne; ++j) {
         const uint32_t e = (uint32_t)(pk >> (9 * j)) & 0x1FFu;
         fn(e & 127u, e >> 7);
