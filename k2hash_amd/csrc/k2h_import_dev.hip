@@ -906,8 +906,12 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   // algorithmic bytes written).  A unit with more than kStageRecs records stores directly.
   // (row kStageRecs: the dump row of the branch-free walk)
   __shared__ __attribute__((aligned(16))) uint64_t s_rec[(kStageRecs + 1) * 4];  // key_off, key_len, val_off, val_len
-  __shared__ __attribute__((aligned(16))) uint64_t s_h[(kStageRecs + 1) * 2];    // h1, h2
-  __shared__ uint8_t s_fk[kStageRecs + 1], s_fv[kStageRecs + 1], s_fh[kStageRecs + 1];  // which parts this unit wrote
+  // the lanes' slot states (3 per lane; round 6: the walk records which slot a key takes, and
+  // the hashes are made from them as they are stored, instead of per event inside the walk)
+  __shared__ uint64_t s_slot[64 * 3];
+  // which parts this unit wrote; s_fh: a key's slot + 1 (its state in s_slot), 0xFF: hashed
+  // from the file, 0: no key of this unit
+  __shared__ uint8_t s_fk[kStageRecs + 1], s_fv[kStageRecs + 1], s_fh[kStageRecs + 1];
   constexpr uint64_t HDR = MDBM ? kHdrRecs : 0;
   const uint64_t base = (uint64_t)blockIdx.x * kUnit;
   const uint64_t blk = blockIdx.x / kUnitsPerBlock;  // pass A's block
@@ -926,7 +930,6 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   // none; slots 0-1 from the packed word, slot 2 -- the third cut's key, when a newline is
   // the event before it -- found from the packed events, round 6)
   const uint32_t te = span_tab<MDBM>(pk);
-  uint64_t sl0 = 0, sl1 = 0, sl2 = 0;
   uint32_t slen = 0xFFFFFFu;
   uint64_t e_lo = 0;
   if constexpr (HASH && !MDBM) e_lo = spec_raw[(uint64_t)kUnitSlots * blockIdx.x + threadIdx.x];
@@ -977,9 +980,9 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       return v;
     };
     const uint32_t p1 = sr.p + sr.v0, p2 = p1 + sr.v1;
-    sl0 = pick(sr.p);  // (all lanes: bpermute reads every lane)
-    sl1 = pick(p1);
-    sl2 = pick(p2);
+    s_slot[3 * threadIdx.x] = pick(sr.p);  // (all lanes: bpermute reads every lane)
+    s_slot[3 * threadIdx.x + 1] = pick(p1);
+    s_slot[3 * threadIdx.x + 2] = pick(p2);
     slen = (sr.p < kUnitSlots ? b0 : 0xFFu) | ((p1 < kUnitSlots ? b1 : 0xFFu) << 8) |
            ((p2 < kUnitSlots ? b2 : 0xFFu) << 16);
   }
@@ -1016,10 +1019,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     for (uint32_t q = threadIdx.x; q < nrec; q += 64) s_fk[q] = s_fv[q] = s_fh[q] = 0;
   __syncthreads();
   bool nulf = s.ln > s.fs;  // a NUL already cut the current field
-  // the slot of this span's next cut event in sl0 and the low byte of slen: both move on at
-  // each cut (a select over three states by a cut counter made hipcc put the walk's
-  // captures in scratch)
-  slen |= 0xFF000000u;
+  uint32_t j = 0;  // cut events of this span so far (slot j's length: byte j of slen)
   typedef uint64_t u64x2 __attribute__((ext_vector_type(2), aligned(8)));  // recs: 8-byte aligned
   auto key_end = [&](uint64_t e) {
     if (s.r < HDR || s.r >= lim) return;
@@ -1033,23 +1033,21 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       *reinterpret_cast<u64x2*>(&recs[r].key_off) = u64x2{s.fs, e - s.fs};
     }
     if constexpr (HASH) {
-      uint64_t a, c;
       // pass A's key for this cut event, if its length is this key's (0xFF: none)
       const uint64_t len = e - s.fs;
-      const uint32_t sj = slen & 0xFFu;
+      const uint32_t sj = j < 3 ? (slen >> (8 * j)) & 0xFFu : 0xFFu;
       const bool hit = sj != 0xFFu && len == sj;
-      const uint64_t raw = sl0;
-      if (hit) {
-        a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
-        c = e > s.fs ? raw : a;
-      } else {  // a state outside the file (never for correct states): wrong records, not a fault
-        hash_cstr_checked(f, size, s.fs, e - s.fs, sp, a, c);
-      }
-      if (staged) {
-        s_h[2 * x] = a;
-        s_h[2 * x + 1] = c;
-        s_fh[x] = 1;
+      if (staged) {  // (hashed as the unit's hashes are stored)
+        s_fh[x] = hit ? 1 + 3 * threadIdx.x + j : 0xFFu;
       } else {
+        uint64_t a, c;
+        if (hit) {
+          const uint64_t raw = s_slot[3 * threadIdx.x + j];
+          a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
+          c = len ? raw : a;
+        } else {  // a state outside the file (never for correct states): wrong records, not a fault
+          hash_cstr_checked(f, size, s.fs, len, sp, a, c);
+        }
         h1[r] = a;
         if (h2) h2[r] = c;
       }
@@ -1102,14 +1100,9 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
       if constexpr (MDBM)
         if (fe && s.m && s.r == 2) val_end(pos, nul);  // the fifth header line's check (record 2 < HDR)
       if constexpr (HASH) {
-        const uint64_t len = pos - s.fs;
-        const uint32_t sj = slen & 0xFFu;
-        const bool hit = sj != 0xFFu && len == sj;
-        const uint64_t raw = sl0;
-        uint64_t a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
-        uint64_t c = pos > s.fs ? raw : a;
-        *reinterpret_cast<u64x2a16*>(&s_h[2 * xk]) = u64x2a16{a, c};
-        s_fh[xk] = ke && !hit ? 2 : 1;  // 2: hashed from the file after the walk
+        const uint32_t sj = j < 3 ? (slen >> (8 * j)) & 0xFFu : 0xFFu;
+        const bool hit = sj != 0xFFu && pos - s.fs == sj;
+        s_fh[xk] = hit ? 1 + 3 * threadIdx.x + j : 0xFFu;  // 0xFF: hashed from the file after the walk
       }
     } else if (fe) {
       if (s.m)
@@ -1121,11 +1114,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     s.fs = brk ? pos + 1 : s.fs;
     nulf = !brk && (nulf || nul);
     s.m = brk ? s.m ^ 1u : s.m;
-    if constexpr (HASH && !MDBM) {  // cut events: TAB and NUL
-      sl0 = nl ? sl0 : sl1;
-      sl1 = nl ? sl1 : sl2;
-      slen = nl ? slen : (slen >> 8) | 0xFF000000u;
-    }
+    j += nl ? 0u : 1u;  // cut events: TAB and NUL
   });
   if (live && base + rel + kTBytes >= size) {  // the thread holding the last byte
     if (s.m && !nulf) val_end(size, false);    // a value read to EOF
@@ -1162,23 +1151,21 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
   // (round 5), one lane per key and few live registers, instead of inside it, where the hash
   // raised the walk's register count (70 VGPRs, 7 waves per SIMD) and serialised the misses
   if constexpr (HASH) {
-    for (uint32_t x = threadIdx.x; x < nrec; x += 64)
-      if (s_fh[x] == 2) {
-        const uint64_t o = s_rec[4 * x], n = s_rec[4 * x + 1];
-        uint64_t a, c;
-        hash_cstr_checked(f, size, o, n, sp, a, c);  // (a wrong state: wrong records, no fault)
-        s_h[2 * x] = a;
-        s_h[2 * x + 1] = c;
-        s_fh[x] = 1;
+    for (uint32_t x = threadIdx.x; x < nrec; x += 64) {
+      const uint32_t code = s_fh[x];
+      if (!code) continue;
+      uint64_t a, c;
+      if (code == 0xFFu) {
+        hash_cstr_checked(f, size, s_rec[4 * x], s_rec[4 * x + 1], sp, a, c);  // (a wrong state: wrong records, no fault)
+      } else {
+        const uint64_t raw = s_slot[code - 1];
+        a = raw * 1099511628211ULL;  // the NUL: a bare multiply (lib/k2hashfunc.cc:56)
+        c = s_rec[4 * x + 1] ? raw : a;
       }
-    __syncthreads();
+      __builtin_nontemporal_store(a, h1 + su.r + x - HDR);
+      if (h2) __builtin_nontemporal_store(c, h2 + su.r + x - HDR);
+    }
   }
-  if constexpr (HASH)
-    for (uint32_t x = threadIdx.x; x < nrec; x += 64)
-      if (s_fh[x]) {
-        __builtin_nontemporal_store(s_h[2 * x], h1 + su.r + x - HDR);
-        if (h2) __builtin_nontemporal_store(s_h[2 * x + 1], h2 + su.r + x - HDR);
-      }
 }
 
 }  // namespace
