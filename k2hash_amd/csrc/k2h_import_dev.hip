@@ -781,8 +781,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
 #pragma unroll
   for (uint32_t h = 0; h < 3; ++h) {
     kk[h] = rk[h] < kUnitSlots ? kk[h] : kNoKey;
-    cls[h] = min((kk[h] >> 16) + 15u, 128u) / 16u;  // 0..8
-    cls[h] = cls[h] ? cls[h] - 1u : 0u;
+    cls[h] = (min(max((kk[h] >> 16) & 0xFFu, 1u), 128u) - 1u) >> 4;  // chunk-count class 0..7
     if (kk[h] != kNoKey) atomicAdd(&s_cls[cls[h]], 1u);
   }
   __syncthreads();
