@@ -219,6 +219,51 @@ __device__ inline TState gapply(const GFn& g, const TState& s) {
   return t;
 }
 
+// lanes of the wave below this one with their bit set in b
+__device__ inline uint32_t lanes_below(uint64_t b) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+}
+
+// Pass B: the state entering each lane's span of a wave (one pass-B unit) whose entry state
+// su is known, and the record ends of the whole unit -- from ballots (round 6), instead of a
+// wave scan of the span functions (hipcub, ~86 VALU per wave) and a gfn_of / gapply per
+// lane.  Positions are unit-relative + 1, as in LFn.  The mode entering lane l is that of
+// the nearest lane below l whose exit mode is fixed (or su.m), flipped by every lane in
+// between that swaps the modes; each lane then takes its own record ends, last boundary and
+// last NUL for its entry mode: the record index is a prefix count (mbcnt of one ballot per
+// bit), the field start and the last NUL the nearest lane below that has one (ds_bpermute).
+__device__ inline TState wave_state_in(const LFn& a, const TState& su, uint64_t base, uint32_t& ends) {
+  const uint32_t l = threadIdx.x & 63u;
+  const uint64_t below = (1ull << l) - 1ull;
+  const uint32_t exk = lfn_mode(a.sel, 0), exv = lfn_mode(a.sel, 1);
+  const uint64_t bfix = __ballot(exk == exv), bk = __ballot(exk != 0), bswap = __ballot(exk != 0 && exv == 0);
+  const uint64_t mf = bfix & below;
+  const uint32_t jf = mf ? 63u - (uint32_t)__builtin_clzll(mf) : 0u;  // (jf < l <= 63)
+  const uint64_t flips = bswap & below & (mf ? ~((2ull << jf) - 1ull) : ~0ull);
+  const uint32_t m = ((mf ? (uint32_t)(bk >> jf) : su.m) ^ (uint32_t)__builtin_popcountll(flips)) & 1u;
+  const uint32_t cnt = (a.cnt >> (16 * m)) & 0xFFFFu, last = (a.last >> (16 * m)) & 0xFFFFu;
+  // record ends below the lane, a ballot per bit (a packed span ends at most 3 records; a
+  // span re-read from the file, up to 64: the wave-uniform test adds the other bits)
+  uint32_t pc = 0;
+  ends = 0;
+  const uint32_t nb = __ballot(cnt > 3u) ? 7u : 2u;
+  for (uint32_t b = 0; b < nb; ++b) {
+    const uint64_t bb = __ballot((cnt >> b) & 1u);
+    pc += lanes_below(bb) << b;
+    ends += (uint32_t)__builtin_popcountll(bb) << b;
+  }
+  const uint64_t hl = __ballot(last != 0) & below, hn = __ballot(a.c != 0) & below;
+  const uint32_t jl = hl ? 63u - (uint32_t)__builtin_clzll(hl) : 0u, jn = hn ? 63u - (uint32_t)__builtin_clzll(hn) : 0u;
+  const uint32_t vl = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(jl << 2), (int)last);  // (every lane)
+  const uint32_t vn = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(jn << 2), (int)a.c);
+  TState t;
+  t.m = m;
+  t.r = su.r + pc;
+  t.fs = hl ? base + vl : su.fs;
+  t.ln = hn ? base + vn : su.ln;  // (a NUL in the unit lies after every position before it)
+  return t;
+}
+
 // Stage block `blk` into lds[PRE + 16 .. PRE + 16 + 16 KiB) with coalesced 16-byte loads
 // (bytes past the file read as 0x01, no event; the 16 bytes below are chunk 0's pad for
 // the hashes), and the PRE bytes before the block into lds[16 .. 16 + PRE) (block 0: 0x01).
@@ -278,12 +323,15 @@ __device__ inline void tsv_stage(const uint8_t* __restrict__ f, uint64_t size, u
 
 // Candidate event bytes (value < 0x0B: NUL, TAB, newline and the rare 0x01-0x08) of a
 // span's 32 words as two 64-bit masks, one bit per byte in byte order.  Each word's
-// candidates are bit 7 of its bytes (three ops); a v_dot4_u32_u8 gathers two words' eight
+// candidates are bit 7 of its bytes (two ops); a v_dot4_u32_u8 gathers two words' eight
 // bits into one byte (multipliers 1, 2, 4, 8 and 16, 32, 64, 128), shifted left by 7.
 // (Round 3: a v_mul_lo_u32 nibble gather per word, a quarter-rate multiply, ~7.7 VALU per
 // word; now ~4.5.)
+// Round 6: two ops per word, not three -- (w - 0x0B0B0B0B) & ~w & 0x80808080 (v_sub, v_bitop3)
+// sets bit 7 of every byte below 0x0B exactly, and of a byte 0x0B whose lower neighbour is
+// below 0x0B (the borrow); such a false candidate has type 0, which every walk skips.
 __device__ inline uint32_t cand_bits(uint32_t w) {
-  return ~(((w & 0x7F7F7F7Fu) + 0x75757575u) | w) & 0x80808080u;  // bit 7 of each byte < 0x0B
+  return (w - 0x0B0B0B0Bu) & ~w & 0x80808080u;  // bit 7 of each byte < 0x0B (+ rare 0x0B)
 }
 __device__ inline void cand_masks(const uint32_t (&w)[32], uint64_t& m0, uint64_t& m1) {
   uint32_t mk[4];
@@ -320,16 +368,22 @@ __device__ inline void tsv_events(const uint8_t* span, uint64_t& m0, uint64_t& m
   }
   uint64_t r0, r1;
   cand_masks(w, r0, r1);
-  // rotate the 128 bits left by 16 s: whole dwords by s / 2, then 16 bits if s is odd
+  // rotate the 128 bits left by 16 s = right by 16 (s & 1), then left by 32 ((s + 1) / 2)
+  // dwords (round 6: the 16-bit step is one alignbit per dword with a per-lane shift of 0 or
+  // 16 -- alignbit(hi, lo, 0) is lo -- instead of an alignbit and a select)
   uint32_t d[4] = {(uint32_t)r0, (uint32_t)(r0 >> 32), (uint32_t)r1, (uint32_t)(r1 >> 32)};
   uint32_t e[4];
-  const bool t2 = s & 4u, t1 = s & 2u, odd = s & 1u;
+  const uint32_t sh = 16u * (s & 1u), q = ((s + 1u) >> 1) & 3u;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) e[i] = t2 ? d[(i + 2) & 3] : d[i];
+  for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_alignbit(d[(i + 1) & 3], d[i], sh);
+  // the dword steps as v_perm with a per-lane selector (bytes of src1 = the other dword, or
+  // of src0 = this one): written as selects, hipcc turned them into a private array indexed
+  // by q -- 32 bytes of scratch per lane, +23 MB of HBM writes per call
+  const uint32_t p2 = (q & 2u) ? 0x03020100u : 0x07060504u, p1 = (q & 1u) ? 0x03020100u : 0x07060504u;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) d[i] = t1 ? e[(i + 3) & 3] : e[i];
+  for (int i = 0; i < 4; ++i) d[i] = __builtin_amdgcn_perm(e[i], e[(i + 2) & 3], p2);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) e[i] = odd ? __builtin_amdgcn_alignbit(d[i], d[(i + 3) & 3], 16) : d[i];
+  for (int i = 0; i < 4; ++i) e[i] = __builtin_amdgcn_perm(d[i], d[(i + 3) & 3], p1);
   m0 = e[0] | ((uint64_t)e[1] << 32);
   m1 = e[2] | ((uint64_t)e[3] << 32);
 }
@@ -361,7 +415,7 @@ template <bool MDBM>
 __device__ inline uint32_t ev_type(uint32_t c) {
   return c < 11u ? ((MDBM ? 0x100003u : 0x180003u) >> (2 * c)) & 3u : 0u;
 }
-// ... of a candidate byte (c < 11, as the masks guarantee)
+// ... of a candidate byte (c <= 11, as the masks guarantee; 11 is the rare false candidate: type 0)
 template <bool MDBM>
 __device__ inline uint32_t cand_type(uint32_t c) {
   return ((MDBM ? 0x100003u : 0x180003u) >> (2 * c)) & 3u;
@@ -522,8 +576,11 @@ constexpr uint32_t kSlots = 2;  // slot states per span on average that a unit's
 // hashes it from the byte after the last newline among them (start < 0, block-relative);
 // before round 4 pass B hashed every such key from the file, one lane holding its wave
 // (~47 us of a 0.62 ms call, profiles/r04d_import_probes.txt).  Block 0's head key starts
-// at the file's first byte.
-constexpr uint32_t kPre = 256;
+// at the file's first byte.  Round 6: 64 bytes, not 256 -- a head key of length L ending at
+// block offset c is found when L <= c + 63 (every key of up to 64 bytes but one ending at
+// offset 0), and the re-read of the bytes before each block drops from 1.6 % of the file to
+// 0.4 %; a longer head key is hashed from the file in pass B.
+constexpr uint32_t kPre = 64;
 constexpr uint32_t kSpecLenMax = 254;  // longest key a slot holds (0xFF: no slot)
 // Each span's slots: the FNV state after the key's bytes (h2 of key + NUL; h1 = raw * P)
 // at raw[kSlots * span + j], written only for the slots its packed word names.
@@ -540,9 +597,6 @@ struct SpecSlots {
 struct SlotRank {
   uint32_t v0, v1, v2, p, n;
 };
-__device__ inline uint32_t lanes_below(uint64_t b) {
-  return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-}
 __device__ inline SlotRank slot_rank(bool v0, bool v1, bool v2) {
   const uint64_t b0 = __ballot(v0), b1 = __ballot(v1), b2 = __ballot(v2);
   return SlotRank{v0 ? 1u : 0u, v1 ? 1u : 0u, v2 ? 1u : 0u, lanes_below(b0) + lanes_below(b1) + lanes_below(b2),
@@ -552,27 +606,75 @@ __device__ inline SlotRank slot_rank(bool v0, bool v1, bool v2) {
 // Newline state of a span for the speculative keys: whether it holds a newline, whether
 // the last one is still open (no cut after it), and its block-relative position; composed
 // in file order (a later newline resets, a cut closes).
-struct NlSum {
-  uint32_t v;  // bit 0: has newline, bit 1: open, bits [2, 18): last newline position
-};
-__device__ inline NlSum nl_compose(NlSum x, NlSum y) {
-  if (y.v & 1u) return y;
-  return NlSum{x.v & ((y.v & 2u) ? ~0u : ~2u)};  // y has no newline; its bit 1 = "no cut in y"
+// (bit 0: has newline, bit 1: open, bits [2, 18): last newline position; identity 2.)
+// compose(x, y) = y if y has a newline, else x with bit 1 cleared when y holds a cut.
+// The block's exclusive prefix from two ballots (round 6; a hipcub block scan before, ~50
+// VALU per wave of DPP steps and selects): a lane's prefix is the state of the nearest lane
+// below it with a newline (fetched by ds_bpermute), closed if a lane in between holds a cut;
+// with none below, the previous wave's aggregate (or the identity), closed likewise.  The
+// waves' aggregates pass through s_agg under one barrier.
+__device__ inline uint32_t nl_prefix_block(uint32_t v, uint32_t* s_agg) {
+  const uint32_t l = threadIdx.x & 63u, w = threadIdx.x >> 6;
+  const uint64_t bnl = __ballot((v & 1u) != 0), bcut = __ballot((v & 2u) == 0);
+  // the wave's aggregate: its last newline lane, closed by a cut in a later lane
+  uint32_t agg = (bcut != 0) ? 0u : 2u;
+  if (bnl) {
+    const uint32_t ja = 63u - (uint32_t)__builtin_clzll(bnl);
+    const uint32_t vj = __builtin_amdgcn_readlane(v, ja);
+    agg = ((bcut >> ja) >> 1) ? (vj & ~2u) : vj;
+  }
+  static_assert(kTThreads == 128, "two waves");
+  if (threadIdx.x == 0) *s_agg = agg;
+  __syncthreads();
+  const uint32_t prev = w ? *s_agg : 2u;
+  const uint64_t below = (1ull << l) - 1ull;
+  const uint64_t m = bnl & below, cb = bcut & below;
+  const uint32_t j = m ? 63u - (uint32_t)__builtin_clzll(m) : 0u;
+  const uint32_t vj = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(j << 2), (int)v);  // (every lane)
+  const bool closed = m ? ((cb >> j) >> 1) != 0 : cb != 0;
+  const uint32_t p = m ? vj : prev;
+  return closed ? (p & ~2u) : p;
 }
-struct NlOp {
-  __device__ uint32_t operator()(uint32_t x, uint32_t y) const { return nl_compose(NlSum{x}, NlSum{y}).v; }
-};
 
-// A wave's function (lane 0's result): pass A needs only the reduction of its span
-// functions (pass B rebuilds the per-span prefixes), so an order-preserving shuffle-down
-// tree -- about half a scan's instructions.  Each wave of pass A writes its own 8 KiB
-// unit's function (round 4: pass B runs one wave per unit, so its scan is a wave scan with
-// no LDS or barrier; round 3 composed the two wave results into a per-block function).
-// (hipcub's warp reduction: DPP row shifts and lane permutes; the round-3 __shfl_down tree
-// compiled to 24 ds_bpermute per lane)
-template <class Tmp>
-__device__ inline LFn wave_fn_reduce(Tmp& tmp, LFn r) {
-  return hipcub::WarpReduce<LFn, 64>(tmp).Reduce(r, LCompose());
+// A wave's function over the whole file (every lane gets it): pass A needs only the
+// composition of its span functions (pass B rebuilds the per-span states), and each wave
+// writes its own 8 KiB unit's (round 4).  Round 6: from ballots, as in wave_state_in, for
+// both entry modes -- each lane's entry mode (the nearest fixed-exit lane below it, flipped
+// by the swapping lanes in between), the record ends summed per bit, the last boundary and
+// NUL taken from the highest lane that has one -- instead of a DPP reduction of the LFn
+// (hipcub WarpReduce, ~60 VALU per wave).  Positions are block-relative + 1.
+__device__ inline GFn wave_gfn(const LFn& a, uint64_t base) {
+  const uint32_t l = threadIdx.x & 63u;
+  const uint64_t below = (1ull << l) - 1ull;
+  const uint32_t exk = lfn_mode(a.sel, 0), exv = lfn_mode(a.sel, 1);
+  const uint64_t bfix = __ballot(exk == exv), bk = __ballot(exk != 0), bswap = __ballot(exk != 0 && exv == 0);
+  const uint64_t mf = bfix & below;
+  const uint32_t jf = mf ? 63u - (uint32_t)__builtin_clzll(mf) : 0u;
+  const uint32_t par = (uint32_t)__builtin_popcountll(bswap & below & (mf ? ~((2ull << jf) - 1ull) : ~0ull)) & 1u;
+  // the lane's entry mode when the wave enters in K (m0) or V (m1)
+  const uint32_t m0 = mf ? ((uint32_t)(bk >> jf) ^ par) & 1u : par, m1 = mf ? m0 : par ^ 1u;
+  const uint32_t c0 = (a.cnt >> (16 * m0)) & 0xFFFFu, c1 = (a.cnt >> (16 * m1)) & 0xFFFFu;
+  const uint32_t l0 = (a.last >> (16 * m0)) & 0xFFFFu, l1 = (a.last >> (16 * m1)) & 0xFFFFu;
+  GFn g = gfn_id();
+  // the exit modes: the wave's last fixed-exit lane, flipped by the swapping lanes after it
+  const uint32_t jw = bfix ? 63u - (uint32_t)__builtin_clzll(bfix) : 0u;
+  const uint32_t pw = (uint32_t)__builtin_popcountll(bswap & (bfix ? ~((2ull << jw) - 1ull) : ~0ull)) & 1u;
+  const uint32_t x0 = bfix ? ((uint32_t)(bk >> jw) ^ pw) & 1u : pw, x1 = bfix ? x0 : pw ^ 1u;
+  g.map = x0 | (x1 << 1);
+  // record ends (a span of at most kEvCap events ends at most 3; more from a longer span)
+  const uint32_t nb = __ballot((c0 | c1) > 3u) ? 7u : 2u;
+  uint64_t n0 = 0, n1 = 0;
+  for (uint32_t b = 0; b < nb; ++b) {
+    n0 += (uint64_t)__builtin_popcountll(__ballot((c0 >> b) & 1u)) << b;
+    n1 += (uint64_t)__builtin_popcountll(__ballot((c1 >> b) & 1u)) << b;
+  }
+  g.cnt0 = n0;
+  g.cnt1 = n1;
+  const uint64_t h0 = __ballot(l0 != 0), h1 = __ballot(l1 != 0), hn = __ballot(a.c != 0);
+  if (h0) g.last0 = base + __builtin_amdgcn_readlane(l0, 63 - __builtin_clzll(h0));
+  if (h1) g.last1 = base + __builtin_amdgcn_readlane(l1, 63 - __builtin_clzll(h1));
+  if (hn) g.lnul = base + __builtin_amdgcn_readlane(a.c, 63 - __builtin_clzll(hn));
+  return g;
 }
 
 // Entry states of the blocks (tsv_scan_kernel, one launch instead of a device scan and a
@@ -656,9 +758,7 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   // 512-byte granule more gave 8 and cost pass A 11 %, round 4.)
   __shared__ uint32_t s_sorted[kTThreads * kSlots];
   __shared__ uint32_t s_cls[8];        // keys per chunk-count class, then class offsets
-  __shared__ typename hipcub::WarpReduce<LFn, 64>::TempStorage s_wred[kTThreads / 64];
-  typedef hipcub::BlockScan<uint32_t, kTThreads, hipcub::BLOCK_SCAN_WARP_SCANS> NlScan;
-  __shared__ typename NlScan::TempStorage tmp;
+  __shared__ uint32_t s_nlagg;  // wave 0's newline aggregate (nl_prefix_block)
   uint8_t* blk = lds + PRE;  // block byte i at blk[16 + i]; the kPre bytes before the block below it
   const uint64_t bid = blockIdx.x;
   if (threadIdx.x < 8) s_cls[threadIdx.x] = 0;
@@ -727,14 +827,13 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     }
     cut0 = (j > 0 && cl[0] < 0) ? cp[0] : cut0;  // (cl[0] < 0: no newline before cut 0 in the span)
   }
-  const LFn wf = wave_fn_reduce(s_wred[threadIdx.x >> 6], acc);
-  if ((threadIdx.x & 63u) == 0) blk_fn[bid * kUnitsPerBlock + (threadIdx.x >> 6)] = gfn_of(wf, base);
+  const GFn wf = wave_gfn(acc, base);
+  if ((threadIdx.x & 63u) == 0) blk_fn[bid * kUnitsPerBlock + (threadIdx.x >> 6)] = wf;
   if constexpr (MDBM) {
     ev[base / kTBytes + threadIdx.x] = pk | kHeadNone;
     return;
   }
-  uint32_t pre_nl;
-  NlScan(tmp).ExclusiveScan(live ? nl : 2u, pre_nl, 2u, NlOp());
+  const uint32_t pre_nl = nl_prefix_block(live ? nl : 2u, &s_nlagg);
   // cut0 ends a key if the state entering the span is a newline with no cut after it
   // (open), or if nothing precedes the span in the block (head: the key started before the
   // block, after the last newline of the kPre bytes before it; block 0: at the file's start)
@@ -800,13 +899,17 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
     if (kk[h] != kNoKey) s_sorted[atomicAdd(&s_cls[cls[h]], 1u)] = kk[h] | (((wv << 7) | rk[h]) << 24);
   __syncthreads();
   const uint32_t nk = s_cls[7];  // (each class's offset has moved to its end: the last is the count)
+  // Right-aligned (round 6): the first round takes the LONGEST min(nk, 128) keys, lane 127
+  // the longest, and a second round the rest (nk > 128), so wave 1 runs the long keys and
+  // wave 0 only the nk - 64 shortest (~49 of ~113 on BASELINE-like files: their chunk count,
+  // not the 64th key's); left-aligned, wave 0 ran keys 0-63 and wave 1 the 49 longest.
   uint64_t raw[2];
   uint32_t slot[2];
 #pragma unroll
   for (uint32_t h = 0; h < 2; ++h) {
-    const uint32_t q = threadIdx.x + h * kTThreads;
+    const uint32_t q = h ? threadIdx.x : threadIdx.x + nk - kTThreads;  // (h = 0: valid from lane 128 - nk)
     slot[h] = 0xFFFFFFFFu;
-    if (q < nk) {
+    if (h ? q + kTThreads < nk : threadIdx.x + nk >= kTThreads) {
       const uint32_t k = s_sorted[q];
       raw[h] = key_raw_lds(blk + 16 + (int16_t)(k & 0xFFFFu), (k >> 16) & 0xFFu, sp);
       slot[h] = k >> 24;
@@ -897,9 +1000,7 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
                                                           k2h_amd_import_rec* __restrict__ recs, SpadTable sp,
                                                           uint64_t* __restrict__ h1, uint64_t* __restrict__ h2,
                                                           uint64_t* __restrict__ hflags) {
-  // one wave per 8 KiB unit: the span functions' prefix is a wave scan (no LDS, no barrier)
-  typedef hipcub::WarpScan<LFn, 64> Scan;
-  __shared__ typename Scan::TempStorage tmp;
+  // one wave per 8 KiB unit: the state entering each span from ballots (wave_state_in)
   // The unit's records, staged in LDS and written out as consecutive 16-byte pieces across
   // the wave (round 4; round 3: each lane stored its own records' halves, 1.31x the
   // algorithmic bytes written).  A unit with more than kStageRecs records stores directly.
@@ -1006,13 +1107,12 @@ __global__ __launch_bounds__(64) void tsv_b_kernel(const uint8_t* __restrict__ f
     acc = lfn_id();
     for_events([&](uint32_t o, uint32_t t) { acc = lfn_push<MDBM>(acc, t, rel + o + 1); });
   }
-  LFn pre, agg;
-  Scan(tmp).ExclusiveScan(acc, pre, lfn_id(), LCompose(), agg);
   const TState su = gapply(ein, tin);  // the state entering the unit
-  TState s = gapply(gfn_of(pre, base), su);
+  uint32_t ends;
+  TState s = wave_state_in(acc, su, base, ends);
   const uint64_t lim = min(count[0], cap) + HDR;  // machine record indices below lim are written
   // the unit touches records su.r .. su.r + (its record ends), the last one possibly in part
-  const uint32_t nrec = (su.m ? agg.cnt >> 16 : agg.cnt & 0xFFFFu) + 1u;
+  const uint32_t nrec = ends + 1u;
   const bool staged = nrec <= kStageRecs;
   if (staged)
     for (uint32_t q = threadIdx.x; q < nrec; q += 64) s_fk[q] = s_fv[q] = s_fh[q] = 0;

@@ -11,7 +11,7 @@ R=$(pwd); O=$R/gpurun_out/${OUT:-import_ab}
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_import.py -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
 tail -1 $O/pytest.txt
-[ -n "$LIBS" ] && { timeout -k 10 300 python3 tools/import_step.py --ab $LIBS ${NOPARITY:+--no-parity} --rounds 7 --calls 10 2>&1 | grep -v Warn | cut -c1-110 || exit 1; }
+[ -n "$LIBS" ] && { timeout -k 10 300 python3 tools/import_step.py --ab $LIBS ${NOPARITY:+--no-parity} --rounds 7 --calls 10 2>&1 | grep -v Warn || exit 1; }
 (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/tree -o run -- python3 $R/tools/import_probe.py > $O/tree.log 2>&1) || { tail $O/tree.log; exit 1; }
 python3 tools/kernel_trace_table.py $O/tree/run_kernel_trace.csv "tsv_" 10 | cut -c1-100
 i=0
