@@ -466,13 +466,15 @@ __device__ inline LFn lfn_push(const LFn& a, uint32_t t, uint32_t p1) {
 // V, [2, 4) / [4, 6) record ends, [6, 9) / [9, 12) boundary index (7: none), [12, 15) the
 // last NUL's index (7: none); TSV, round 6: [15, 18), [18, 21), [21, 24) the index of the
 // span's cut 0, 1, 2 when the event before it is a newline -- the in-span keys pass A
-// hashes for slots 0-2 (7: none); [24, 27) the number of events.
+// hashes for slots 0-2 (7: none); [24, 27) the number of events; round 6, for pass A's
+// newline state: [27, 30) the index of the last newline (7: none), bit 30 a cut (TAB / NUL)
+// after it (or, with no newline, anywhere in the span).
 template <bool MDBM>
 struct SpanTab {
   uint32_t v[4096];
   constexpr SpanTab() : v() {
     for (uint32_t s = 0; s < 4096; ++s) {
-      uint32_t out = 0, nul = 7, ins[3] = {7, 7, 7}, ncut = 0, prev = 0, ne = 0;
+      uint32_t out = 0, nul = 7, ins[3] = {7, 7, 7}, ncut = 0, prev = 0, ne = 0, lnl = 7, cut_after = 0;
       for (uint32_t m = 0; m < 2; ++m) {
         uint32_t mode = m, cnt = 0, last = 7;
         for (uint32_t i = 0; i < kEvCap; ++i) {
@@ -496,9 +498,12 @@ struct SpanTab {
           ++ncut;
         }
         ne += t ? 1u : 0u;
+        if (t == 1u) lnl = i, cut_after = 0;
+        if (t >= 2u) cut_after = 1;
         prev = t;
       }
-      v[s] = out | (nul << 12) | (ins[0] << 15) | (ins[1] << 18) | (ins[2] << 21) | (ne << 24);
+      v[s] = out | (nul << 12) | (ins[0] << 15) | (ins[1] << 18) | (ins[2] << 21) | (ne << 24) | (lnl << 27) |
+             (cut_after << 30);
     }
   }
 };
@@ -772,60 +777,51 @@ __global__ __launch_bounds__(kTThreads) void tsv_a_kernel(const uint8_t* __restr
   // (round 6: one 64-bit shift per event instead of a variable shift and two guards); a span
   // of ne <= kEvCap events holds them at [54 - 9 ne, 54) after the walk, shifted down then
   uint64_t pk = 0;
-  uint32_t ne = 0, nl = 2u;  // nl: no newline yet, and "no cut seen" (bit 1) until one is
-  // Speculative keys, found in the same walk (round 4; round 3 walked the packed events a
-  // second time after the block scan): a cut that follows a newline of this span ends the
-  // key that starts after it; the span's first cut, if no newline precedes it here, waits
-  // for the scan (cut0) -- the entering state decides whether it ends a key, and where
-  // that key starts.  The walk only records the span's first two cuts with the newline
-  // state they met; the keys are assembled after it (round 5: a wave walks as many events
-  // as its busiest lane, so per-event instructions cost 2.5x their mean share).
-  uint32_t j = 0;                     // cut events so far
-  // cut h's position (bits 0-13) and the newline state it met (bits 14-29: nl before the
-  // cut; round 6: the last newline since the previous cut, and whether one preceded cut 0,
-  // read from it after the walk instead of being tracked per event)
-  uint32_t cw[3] = {0, 0, 0};  // (cut 2: the in-span key pass A hashes for slot 2, round 6)
+  uint32_t ne = 0;
+  // Speculative keys (round 4; round 3 walked the packed events a second time after the
+  // block scan): a cut that follows a newline of this span ends the key that starts after
+  // it; the span's first cut, if no newline precedes it here, waits for the scan (cut0) --
+  // the entering state decides whether it ends a key, and where that key starts.  Round 6:
+  // the walk only packs the events (a wave walks as many as its busiest lane, 2.5x the mean,
+  // so each per-event instruction counts 2.5 times); the cuts, their keys and the span's
+  // newline state are read off the packed word and its span_tab entry after the walk (a
+  // span of more than kEvCap events names no key and reports no newline: only misses).
   constexpr uint32_t kNoKey = 0xFFFFFFFFu;
   uint32_t key0 = kNoKey, key1 = kNoKey, key2 = kNoKey;  // the span's keys at cuts 0-2: start | len << 16
   if (live)
     span_events<MDBM>(span, [&](uint32_t o, uint32_t t) {  // branch-free: t == 0 changes nothing
-      acc = lfn_push<MDBM>(acc, t, rel + o + 1);
       // (selects throughout: the branches hipcc made of these cost ~40 SALU per event)
       pk = t ? (pk >> 9) | ((uint64_t)(o | (t << 7)) << 45) : pk;
       ne += t ? 1u : 0u;
-      if constexpr (!MDBM) {
-        const bool cut = t >= 2u;  // TAB or NUL
-        const uint32_t w = (rel + o) | (nl << 14);
-        cw[0] = (cut && j == 0) ? w : cw[0];
-        cw[1] = (cut && j == 1) ? w : cw[1];
-        cw[2] = (cut && j == 2) ? w : cw[2];
-        j += cut ? 1u : 0u;
-      }
-      const uint32_t nlv = 3u | ((rel + o) << 2), nlc = nl & (t ? ~2u : ~0u);
-      nl = t == 1u ? nlv : nlc;
     });
   const bool over = ne > kEvCap;
   pk = over ? kEvOver : pk >> (9 * (kEvCap - ne));
+  // The span's function by table from the packed word, as pass B builds it (round 6; the
+  // walk composed it per event, ~12 VALU each); a span of more than kEvCap events (rare)
+  // walks its candidates again for it.
+  const uint32_t te = span_tab<MDBM>(pk);
+  acc = lfn_of_packed<MDBM>(pk, rel, te);
+  if (over) {
+    acc = lfn_id();
+    span_events<MDBM>(span, [&](uint32_t o, uint32_t t) { acc = lfn_push<MDBM>(acc, t, rel + o + 1); });
+  }
   uint32_t head_len = 0xFFu;  // the head key's length byte
   uint32_t cut0 = 0xFFFFFFFFu;  // the span's first cut when no newline precedes it
+  uint32_t nl = 2u;  // newline state (NlSum): no newline, no cut
   if constexpr (!MDBM) {
-    int32_t cl[3];  // the last newline before cut h with no cut between them (-1: none)
-    uint32_t cp[3];
+    auto off = [&](uint32_t i) { return (uint32_t)(pk >> (9 * i)) & 127u; };
+    uint32_t kk[3];
 #pragma unroll
     for (uint32_t h = 0; h < 3; ++h) {
-      const uint32_t nlp = cw[h] >> 14;
-      cp[h] = cw[h] & 0x3FFFu;
-      cl[h] = (nlp & 3u) == 3u ? (int32_t)(nlp >> 2) : -1;
-      const uint32_t len = cp[h] - (uint32_t)(cl[h] + 1);
-      // (no length byte: pass B finds these keys from the packed events, so none for a span
-      // past kEvCap; in-span, len < 128)
-      const bool em = j > h && cl[h] >= 0 && !over;
-      const uint32_t k = ((uint32_t)(cl[h] + 1) & 0xFFFFu) | (len << 16);
-      if (h == 0) key0 = em ? k : kNoKey;
-      else if (h == 1) key1 = em ? k : kNoKey;
-      else key2 = em ? k : kNoKey;
+      const uint32_t x = (te >> (15 + 3 * h)) & 7u;  // cut h's event, a newline before it (7: none)
+      const uint32_t st = off(x - 1u) + 1u;             // (x >= 1 when named)
+      // (no length byte: pass B finds these keys from the packed events; in-span, len < 128)
+      kk[h] = (x != 7u && !over) ? (rel + st) | ((off(x) - st) << 16) : kNoKey;
     }
-    cut0 = (j > 0 && cl[0] < 0) ? cp[0] : cut0;  // (cl[0] < 0: no newline before cut 0 in the span)
+    key0 = kk[0], key1 = kk[1], key2 = kk[2];
+    cut0 = (!over && ne && (pk & 0x100u)) ? rel + off(0) : cut0;  // event 0 a cut (type >= 2: bit 8)
+    const uint32_t lx = (te >> 27) & 7u, ca = (te >> 30) & 1u;
+    nl = over ? 0u : lx != 7u ? 1u | (ca ? 0u : 2u) | ((rel + off(lx)) << 2) : (ca ? 0u : 2u);
   }
   const GFn wf = wave_gfn(acc, base);
   if ((threadIdx.x & 63u) == 0) blk_fn[bid * kUnitsPerBlock + (threadIdx.x >> 6)] = wf;
