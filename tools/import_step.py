@@ -61,11 +61,13 @@ def main():
                     "the digest check (their results may be wrong by design)")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
+    if a.lib:
+        _native._batch = _native._bind(ctypes.CDLL(str(Path(a.lib).resolve())), _native.SIGNATURES.keys())
     if a.mdbm:  # one verified call, then the timed calls
         data, exp = mdbm_workload(dev)
         ok = verify_mdbm(archive.import_scan_prehash_device(data, "mdbm"), data, exp)
         print(json.dumps({"mdbm_bytes": data.numel(), "records": int(exp.shape[0]), "verify_ok": ok}), flush=True)
-        if not ok:
+        if not ok and not a.no_parity:
             sys.exit(1)
         t0 = time.perf_counter()
         while time.perf_counter() - t0 < 0.15:
@@ -81,8 +83,6 @@ def main():
         print(json.dumps({"mdbm_ms_per_call_median": statistics.median(ts), "min": min(ts), "all": ts}))
         return
     data = bench.import_workload(dev)
-    if a.lib:
-        _native._batch = _native._bind(ctypes.CDLL(str(Path(a.lib).resolve())), _native.SIGNATURES.keys())
     if a.ab:
         libs = {"tree": _native.batch_lib()}
         for p in a.ab.split(","):
