@@ -191,17 +191,6 @@ struct GCompose {
     return r;
   }
 };
-__device__ inline GFn gfn_of(const LFn& l, uint64_t base) {
-  GFn g;
-  g.map = lfn_mode(l.sel, 0) | (lfn_mode(l.sel, 1) << 1);
-  g.pad = 0;
-  g.cnt0 = l.cnt & 0xFFFFu;
-  g.cnt1 = l.cnt >> 16;
-  g.last0 = (l.last & 0xFFFFu) ? base + (l.last & 0xFFFFu) : 0;
-  g.last1 = (l.last >> 16) ? base + (l.last >> 16) : 0;
-  g.lnul = l.c ? base + l.c : 0;
-  return g;
-}
 
 struct TState {
   uint32_t m;   // mode (1 = V)
